@@ -1,0 +1,250 @@
+"""Benchmark: training-step spectrogram-frames/s (BASELINE.json metric), MI355X.
+
+Workload (BASELINE.json configs[2] / SURVEY 8(d) config 3): one PerformanceNet training
+step per GPU on a batch of 32 synthetic 4 s @ 16 kHz piano clips (L = 64,256 samples,
+T = 252 frames): on-the-fly STFT log-power front end of the target clips and of the
+style-reference clips (preprocess.py:47-49) -> PerformanceNet forward (model.py:262-300)
+-> L1 loss -> backward -> [RCCL gradient all-reduce when N > 1] -> Adam(lr=1e-3)
+(train.py:129-143). Dropout on (train mode). Everything inside the timed region runs in
+libmst_hip kernels; inputs are resident in HBM before timing starts.
+
+value = (N * 32 * 252) frames / (max over ranks of the timed wall time / K steps).
+
+Launch: python bench.py [--gpus 1] [--steps K] [--warmup W]; N > 1 under
+torch.distributed.run (one rank per GPU, RCCL). Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SR = 16000
+HOP = 256
+T_FRAMES = 252                      # 4.016 s: T = 12 (mod 16) so the U-Net round-trips
+L_SAMPLES = HOP * (T_FRAMES - 1)    # 64,256
+PEAK_FP32_MFMA = 157.3              # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = vector rate)
+
+
+def synth_clips(n, seed0, L=L_SAMPLES, sr=SR):
+    """SURVEY 8(d) synthetic piano clips: Poisson onsets (~4 notes/s), pitch U{21..108},
+    duration U[0.1,1] s, velocity U[0.3,1], 8 harmonics 0.6^h, exp(-3t) decay, peak 0.5."""
+    clips, notes_all = [], []
+    t = np.arange(L) / sr
+    for c in range(n):
+        rng = np.random.RandomState(seed0 + c)
+        dur_total = L / sr
+        k = max(1, rng.poisson(4 * dur_total))
+        notes = []
+        y = np.zeros(L)
+        for _ in range(k):
+            on = rng.uniform(0, dur_total)
+            pitch = rng.randint(21, 109)
+            d = rng.uniform(0.1, 1.0)
+            vel = rng.uniform(0.3, 1.0)
+            f0 = 440.0 * 2 ** ((pitch - 69) / 12)
+            tt = t - on
+            m = (tt >= 0) & (tt < d + 0.5)
+            env = np.exp(-3 * tt[m])
+            for h in range(1, 9):
+                if h * f0 < sr / 2:
+                    y[m] += vel * 0.6 ** h * np.sin(2 * np.pi * h * f0 * tt[m]) * env
+            notes.append((pitch, on, min(on + d, dur_total), vel))
+        peak = np.abs(y).max()
+        clips.append((0.5 * y / peak if peak > 0 else y).astype(np.float32))
+        notes_all.append(notes)
+    return np.stack(clips), notes_all
+
+
+def piano_rolls(notes_all, T=T_FRAMES, wps=SR // HOP):
+    """pretty_midi-style roll at fs = wps (preprocess.py:147-155), binarised; onoff = diff."""
+    rolls = np.zeros((len(notes_all), 128, T), np.float32)
+    for i, notes in enumerate(notes_all):
+        for p, s, e, _ in notes:
+            rolls[i, p, int(s * wps):int(e * wps)] = 1
+    prev = np.concatenate([np.zeros_like(rolls[:, :, :1]), rolls[:, :, :-1]], 2)
+    return rolls, rolls - prev
+
+
+def cpu_baseline(B=4, steps=2):
+    """The oracle's torch-CPU restatement of the reference training step (oracle/model_ref.py),
+    timed on this host: bounded sample of B clips x T=252, `steps` timed steps after 1 warmup."""
+    from oracle import model_ref as R
+    from oracle import detinit
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    p = R.det_params()
+    for v in p.values():
+        v.requires_grad_(True)
+    xm, xa, cd, tg = (torch.from_numpy(a) for a in detinit.model_inputs(B, T_FRAMES))
+    state = {}
+
+    def step(i):
+        for v in p.values():
+            v.grad = None
+        y = R.forward(p, xm, xa, cd, train=True)
+        loss = R.l1_loss(y, tg)
+        loss.backward()
+        with torch.no_grad():
+            R.adam_step(p, {k: v.grad for k, v in p.items() if not k.startswith("MBR")}, state, i + 1)
+        return loss.item()
+
+    step(0)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i + 1)
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(B * T_FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{steps} timed train steps (fwd+L1+bwd+Adam) of oracle/model_ref.py on "
+                      f"torch-CPU, B={B}, T={T_FRAMES}, {threads} threads ({dt:.2f} s/step)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kernel-timing-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from ml_music_style_transfer_amd import dp, spectral
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd import kernels as K
+    from ml_music_style_transfer_amd.model import PerformanceNet
+    from ml_music_style_transfer_amd.train import make_optimizer
+
+    B = args.batch
+    torch.manual_seed(1234)
+    model = PerformanceNet().to(dev)
+    model.train()
+    dp.broadcast_parameters(model)
+    opt = make_optimizer(model, lr=1e-3)
+
+    # synthetic per-rank data, resident in HBM: target clips, style-reference clips, rolls
+    tgt_audio, notes = synth_clips(B, 1234 + 1000 * rank)
+    ref_audio, _ = synth_clips(B, 777_000 + 1000 * rank)
+    roll, onoff = piano_rolls(notes)
+    tgt_audio = torch.from_numpy(tgt_audio).to(dev)
+    ref_audio = torch.from_numpy(ref_audio).to(dev)
+    data = torch.from_numpy(np.concatenate([roll, onoff], 1)).to(dev)  # (B, 256, T) train.py:84-85
+
+    def step():
+        opt.zero_grad()
+        target = spectral.stft_logpow(tgt_audio, hop=HOP)           # (B, 1025, 252)
+        x_audio = spectral.stft_logpow(ref_audio, hop=HOP)          # style reference spec
+        split = torch.split(data, 128, dim=1)                      # train.py:130
+        y = model(split[0], x_audio, split[1])
+        loss = E.l1_loss(y, target)
+        loss.backward()
+        dp.allreduce_gradients(model)
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = tt.item()
+    ms_per_step = 1000.0 * dt / args.steps
+    value = world * B * T_FRAMES / (dt / args.steps)
+    final_loss = loss.item()
+
+    # roofline leg: per-launch HIP events around every GEMM (fp32 MFMA implicit GEMM) of a few
+    # extra steps, on the launch stream; achieved = algorithmic FLOPs / summed kernel time.
+    log = []
+    K.gemm_timing(log)
+    for _ in range(args.kernel_timing_steps):
+        step()
+    K.gemm_timing(None)
+    torch.cuda.synchronize()
+    gemm_ms = sum(s.elapsed_time(e) for s, e, _, _ in log)
+    gemm_flops = sum(f for _, _, f, _ in log)
+    n_steps_t = max(1, args.kernel_timing_steps)
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    by_tag = {}
+    for s, e, f, tag in log:
+        a = by_tag.setdefault(tag, [0.0, 0.0, 0])
+        a[0] += s.elapsed_time(e)
+        a[1] += f
+        a[2] += 1
+
+    out = {
+        "metric": "training-step spectrogram-frames/sec, batch 32, 4 s @ 16 kHz, 1/2/4/8 GPUs",
+        "value": round(value, 1),
+        "unit": "spectrogram-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (16 kHz piano clips per SURVEY 8(d); random-init PerformanceNet weights)",
+        "config": {"workload": "PerformanceNet train step: STFT front end + fwd + L1 + bwd"
+                               + (" + RCCL all-reduce" if world > 1 else "") + " + Adam",
+                   "global_batch": world * B, "batch_per_gpu": B, "seq_len": T_FRAMES,
+                   "sample_rate": SR, "n_fft": 2048, "hop": HOP, "parallelism": f"dp{world}"},
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "gemm_kernel (fp32 MFMA 32x32x2 implicit GEMM, all conv/linear fwd/dgrad/wgrad)",
+            "achieved": round(achieved, 2),
+            "peak": PEAK_FP32_MFMA,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_FP32_MFMA, 4),
+            "traffic": None,
+            "gemm_gflop_per_step": round(gemm_flops / n_steps_t / 1e9, 1),
+            "gemm_ms_per_step": round(gemm_ms / n_steps_t, 3),
+            "launches_per_step": len(log) // n_steps_t,
+            "by_kind": {k: {"ms_per_step": round(v[0] / n_steps_t, 3),
+                            "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] else 0}
+                        for k, v in by_tag.items()},
+        },
+        "final_loss": round(final_loss, 5),
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

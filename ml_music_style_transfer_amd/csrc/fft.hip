@@ -1,0 +1,616 @@
+// Spectral front end on gfx950: STFT (log-power / power / mel / complex), iSTFT and
+// Griffin-Lim for n_fft = 2048 (the reference's only FFT size: preprocess.py:25,48;
+// inference.py:105-110; test_griffinlim.py:23).
+//
+// FFT design: a real 2048-point frame is packed as a 1024-point complex signal
+// z[n] = x[2n] + i x[2n+1] (window applied on load). One wave owns one frame; each lane
+// holds 16 complex values and the 1024-point FFT runs as radix-16 (registers) ->
+// LDS transpose -> radix-16 (registers) -> LDS transpose -> radix-4, then the real-FFT
+// post-twist (X[k] from Z[k], Z[1024-k]) produces the 1025 bins. Row strides of the LDS
+// images are padded (68 complex) so every ds_read/ds_write_b64 lane group is
+// conflict-free. Twiddles come from a 512-entry quarter-wave LDS table
+// (W^(512q + r) = (-i)^q W^r), built in double precision on the host side of the
+// compiler (constexpr-free: computed once per workgroup with sincospi in f64).
+//
+// STFT workgroups: 512 threads (8 waves) x 32 frames of one clip. Results are staged
+// through LDS (reusing the FFT scratch) so each (bin, 32 frames) row of the (B, F, T)
+// output is written as one 128-byte run.
+#include "common.h"
+
+namespace {
+
+constexpr int NFFT = 2048;
+constexpr int NC = 1024;        // complex FFT length
+constexpr int NB = NC + 1;      // output bins
+constexpr int RS = 68;          // padded LDS row stride (complex) for the 16 x 64 images
+constexpr int SCR = 16 * RS;    // complex per wave scratch (1088)
+constexpr int WAVES = 8;
+constexpr int FR = 32;          // frames per STFT workgroup
+constexpr int QT = 512;         // quarter-wave twiddle table entries
+
+struct c2 {
+  float x, y;
+};
+__device__ __forceinline__ c2 mk(float x, float y) { return c2{x, y}; }
+__device__ __forceinline__ c2 operator+(c2 a, c2 b) { return mk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ c2 operator-(c2 a, c2 b) { return mk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ c2 operator*(c2 a, float s) { return mk(a.x * s, a.y * s); }
+__device__ __forceinline__ c2 cmul(c2 a, c2 b) {
+  return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ c2 conj(c2 a) { return mk(a.x, -a.y); }
+
+// W_2048^k (forward: exp(-2 pi i k / 2048)); INV conjugates.
+template <bool INV>
+__device__ __forceinline__ c2 tw(const c2* qt, int k) {
+  k &= (NFFT - 1);
+  int q = k >> 9, r = k & (QT - 1);
+  c2 w = qt[r];  // (cos, -sin) of 2 pi r / 2048
+  c2 o;
+  // multiply by (-i)^q
+  if (q == 0) o = w;
+  else if (q == 1) o = mk(w.y, -w.x);
+  else if (q == 2) o = mk(-w.x, -w.y);
+  else o = mk(-w.y, w.x);
+  if (INV) o.y = -o.y;
+  return o;
+}
+
+__device__ void build_qtable(c2* qt) {
+  for (int r = threadIdx.x; r < QT; r += blockDim.x) {
+    double s, c;
+    sincospi((double)r / 1024.0, &s, &c);
+    qt[r] = mk((float)c, (float)-s);
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
+  c2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
+  c2 it3 = mk(-t3.y, t3.x);  // i * t3
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  if (!INV) {
+    a1 = t1 - it3;
+    a3 = t1 + it3;
+  } else {
+    a1 = t1 + it3;
+    a3 = t1 - it3;
+  }
+}
+
+// W16^m as compile-time constants (forward sign).
+__device__ __forceinline__ c2 w16(int m) {
+  constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654752f;
+  switch (m & 15) {
+    case 0: return mk(1.f, 0.f);
+    case 1: return mk(C1, -S1);
+    case 2: return mk(R2, -R2);
+    case 3: return mk(S1, -C1);
+    case 4: return mk(0.f, -1.f);
+    case 5: return mk(-S1, -C1);
+    case 6: return mk(-R2, -R2);
+    case 7: return mk(-C1, -S1);
+    case 8: return mk(-1.f, 0.f);
+    case 9: return mk(-C1, S1);
+    default: return mk(0.f, 0.f);  // not needed (j1*k2 <= 9)
+  }
+}
+
+// In-register 16-point DFT: out[k] = sum_j v[j] W16^{jk} (INV: conjugate twiddles).
+template <bool INV>
+__device__ __forceinline__ void dft16(c2 v[16]) {
+#pragma unroll
+  for (int j1 = 0; j1 < 4; ++j1) dft4<INV>(v[j1], v[j1 + 4], v[j1 + 8], v[j1 + 12]);
+  // v[j1 + 4 k2] = Y[j1][k2]; twiddle by W16^{j1 k2}
+#pragma unroll
+  for (int j1 = 1; j1 < 4; ++j1)
+#pragma unroll
+    for (int k2 = 1; k2 < 4; ++k2) {
+      c2 w = w16(j1 * k2);
+      if (INV) w.y = -w.y;
+      v[j1 + 4 * k2] = cmul(v[j1 + 4 * k2], w);
+    }
+  // DFT4 over j1 for each k2: X[k2 + 4 k1] = sum_j1 W4^{j1 k1} Y[j1][k2]
+#pragma unroll
+  for (int k2 = 0; k2 < 4; ++k2) dft4<INV>(v[4 * k2], v[4 * k2 + 1], v[4 * k2 + 2], v[4 * k2 + 3]);
+  // now v[j1' + 4 k2] holds X[k2 + 4 k1] with k1 = j1' -> transpose 4x4 into natural order
+  c2 t[16];
+#pragma unroll
+  for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) t[k2 + 4 * k1] = v[k1 + 4 * k2];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = t[i];
+}
+
+// 1024-point complex FFT of one wave. Input v[j] = z[lane + 64 j]; on return S[k]
+// (k = 0..1023, natural order, unnormalised) holds Z[k]. S: this wave's scratch.
+template <bool INV>
+__device__ void fft1024(c2 v[16], c2* S, const c2* qt, int lane) {
+  // pass A: radix-16 over j, twiddle W1024^{lane k1} = W2048^{2 lane k1}
+  dft16<INV>(v);
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw<INV>(qt, 2 * lane * k1));
+#pragma unroll
+  for (int k1 = 0; k1 < 16; ++k1) S[k1 * RS + lane] = v[k1];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // pass B: lane = k1*4 + lp; 16-point DFT over jp of X1[k1][lp + 4 jp]
+  {
+    const int k1 = lane >> 2, lp = lane & 3;
+#pragma unroll
+    for (int jp = 0; jp < 16; ++jp) v[jp] = S[k1 * RS + lp + 4 * jp];
+    dft16<INV>(v);
+#pragma unroll
+    for (int mp = 1; mp < 16; ++mp) v[mp] = cmul(v[mp], tw<INV>(qt, 32 * lp * mp));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int mp = 0; mp < 16; ++mp) S[k1 * RS + mp * 4 + lp] = v[mp];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  // pass C: (k1 = lane & 15, mp = (lane >> 4) + 4 q), 4-point DFT over lp
+  {
+    const int k1 = lane & 15;
+    c2 c[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mp = (lane >> 4) + 4 * q;
+#pragma unroll
+      for (int lp = 0; lp < 4; ++lp) c[q][lp] = S[k1 * RS + mp * 4 + lp];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int mp = (lane >> 4) + 4 * q;
+      dft4<INV>(c[q][0], c[q][1], c[q][2], c[q][3]);
+#pragma unroll
+      for (int m2 = 0; m2 < 4; ++m2) S[k1 + 16 * mp + 256 * m2] = c[q][m2];
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ float hann_w(const c2* qt, int n) {
+  // 0.5 - 0.5 cos(2 pi n / 2048), periodic Hann (scipy get_window('hann', 2048, fftbins=True))
+  return 0.5f - 0.5f * tw<false>(qt, n).x;
+}
+
+// Frame f of clip xr (length L): lanes load the windowed packed input z[lane + 64 j].
+__device__ __forceinline__ void load_frame(const float* xr, int L, int f, int hop, int pad_mode,
+                                           const c2* qt, int lane, c2 v[16]) {
+  const int s0 = f * hop - NFFT / 2;
+  const bool interior = s0 >= 0 && s0 + NFFT <= L && ((((uintptr_t)(xr + s0)) & 7) == 0);
+  if (interior) {
+    const float2* p = reinterpret_cast<const float2*>(xr + s0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      int n = lane + 64 * j;
+      float2 e = p[n];
+      v[j] = mk(e.x * hann_w(qt, 2 * n), e.y * hann_w(qt, 2 * n + 1));
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      int n = lane + 64 * j;
+      float e[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int s = s0 + 2 * n + h;
+        float val;
+        if (s >= 0 && s < L) val = xr[s];
+        else if (pad_mode == MST_PAD_CONSTANT) val = 0.f;
+        else {
+          if (s < 0) s = -s;
+          if (s >= L) s = 2 * (L - 1) - s;
+          val = (s >= 0 && s < L) ? xr[s] : 0.f;
+        }
+        e[h] = val * hann_w(qt, 2 * n + h);
+      }
+      v[j] = mk(e[0], e[1]);
+    }
+  }
+}
+
+// Real-FFT post-twist: X[k] for k = lane + 64 j from Z in S; X[1024] via lane 0.
+__device__ __forceinline__ c2 post_bin(const c2* S, const c2* qt, int k) {
+  c2 A = S[k];
+  c2 Bc = conj(S[(NC - k) & (NC - 1)]);
+  c2 xe = (A + Bc) * 0.5f;
+  c2 d = A - Bc;
+  c2 xo = mk(0.5f * d.y, -0.5f * d.x);  // -i/2 * d
+  return xe + cmul(tw<false>(qt, k), xo);
+}
+
+__device__ __forceinline__ float log1p_fast(float p) {
+  // log1p via log(u) * p / (u - 1) (exact-ish for tiny p), hardware log2
+  float u = 1.f + p;
+  float d = u - 1.f;
+  float l = __log2f(u) * 0.69314718055994531f;
+  return d == 0.f ? p : l * (p / d);
+}
+
+enum { MODE_LOGPOW = 0, MODE_POWER = 1, MODE_MEL = 2, MODE_COMPLEX = 3 };
+
+struct MelTab {
+  const int* start;
+  const int* len;
+  const int* woff;
+  const float* w;
+  int n_mels;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(512, 1) void stft_kernel(const float* __restrict__ x, int L, int T,
+                                                      int hop, int pad_mode,
+                                                      float* __restrict__ out, MelTab mel) {
+  __shared__ __attribute__((aligned(16))) c2 scratch[WAVES * SCR];
+  __shared__ c2 qt[QT];
+  const int b = blockIdx.y;
+  const int f0 = blockIdx.x * FR;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  build_qtable(qt);
+  __syncthreads();
+  const float* xr = x + (long long)b * L;
+  c2* S = scratch + wave * SCR;
+
+  constexpr int NR = (MODE == MODE_MEL) ? 2 : 17;
+  float res[4][NR];
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int f = f0 + wave + WAVES * i;
+    if (f < T) {
+      c2 v[16];
+      load_frame(xr, L, f, hop, pad_mode, qt, lane, v);
+      fft1024<false>(v, S, qt, lane);
+      if (MODE == MODE_COMPLEX) {
+        float2* o = reinterpret_cast<float2*>(out) + ((long long)b * T + f) * NB;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          int k = lane + 64 * j;
+          c2 X = post_bin(S, qt, k);
+          o[k] = make_float2(X.x, X.y);
+        }
+        if (lane == 0) {
+          c2 z0 = S[0];
+          o[NC] = make_float2(z0.x - z0.y, 0.f);
+        }
+      } else if (MODE == MODE_MEL) {
+        // power spectrum -> this wave's scratch as floats, then 2 bands per lane
+        float P[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          c2 X = post_bin(S, qt, lane + 64 * j);
+          P[j] = X.x * X.x + X.y * X.y;
+        }
+        float pn = 0.f;
+        if (lane == 0) {
+          c2 z0 = S[0];
+          float xn = z0.x - z0.y;
+          pn = xn * xn;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        float* Pf = reinterpret_cast<float*>(S);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) Pf[lane + 64 * j] = P[j];
+        if (lane == 0) Pf[NC] = pn;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          int m = lane + 64 * h;
+          float acc = 0.f;
+          if (m < mel.n_mels) {
+            int s = mel.start[m], n = mel.len[m], wo = mel.woff[m];
+            for (int q = 0; q < n; ++q) acc += mel.w[wo + q] * Pf[s + q];
+          }
+          res[i][h] = acc;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          c2 X = post_bin(S, qt, lane + 64 * j);
+          float p = X.x * X.x + X.y * X.y;
+          res[i][j] = (MODE == MODE_LOGPOW) ? log1p_fast(p) : p;
+        }
+        c2 z0 = S[0];
+        float xn = z0.x - z0.y;
+        float p = xn * xn;
+        res[i][16] = (MODE == MODE_LOGPOW) ? log1p_fast(p) : p;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  if (MODE == MODE_COMPLEX) return;
+
+  // ---- stage through LDS and write (bin, 32-frame) rows ----
+  __syncthreads();
+  float* stage = reinterpret_cast<float*>(scratch);
+  constexpr int SST = FR + 1;
+  const int nfr = min(FR, T - f0);
+  if (MODE == MODE_MEL) {
+    const int nm = mel.n_mels;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int fl = wave + WAVES * i;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int m = lane + 64 * h;
+        if (m < nm && fl < nfr) stage[m * SST + fl] = res[i][h];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nm * FR; e += blockDim.x) {
+      int m = e / FR, fl = e - m * FR;
+      if (fl < nfr) out[((long long)b * nm + m) * T + f0 + fl] = stage[m * SST + fl];
+    }
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int fl = wave + WAVES * i;
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        int kr = lane + 64 * jj;  // bin within this round
+        if (fl < nfr) stage[kr * SST + fl] = res[i][4 * r + jj];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 256 * FR; e += blockDim.x) {
+      int kr = e / FR, fl = e - kr * FR;
+      if (fl < nfr) out[((long long)b * NB + 256 * r + kr) * T + f0 + fl] = stage[kr * SST + fl];
+    }
+    __syncthreads();
+  }
+  // bin 1024
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int fl = wave + WAVES * i;
+      if (fl < nfr) stage[fl] = res[i][16];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < nfr) out[((long long)b * NB + NC) * T + f0 + threadIdx.x] = stage[threadIdx.x];
+}
+
+// ---------------------------------------------------------------------------
+// iSTFT (librosa.istft, center=True, Hann): workgroup = 512 threads, output segment of
+// SEG = 16 samples per thread. Frames overlapping the segment are inverse-FFT'd 8 at a
+// time (one per wave) into the waves' scratch; every thread then accumulates its own
+// samples frame by frame in increasing frame order (deterministic OLA), together with
+// the window-sum-square, and divides at the end.
+//
+// Spectrum input is frame-major complex (B, T, F, 2). With `prev` the spectrum used is
+// normalise(cur - beta*prev) (Griffin-Lim momentum, librosa.griffinlim); with `mag`
+// (B, T, F) it is multiplied by the magnitude; cur == NULL means all-ones phases.
+// ---------------------------------------------------------------------------
+constexpr int ISEG = 512 * 16;
+
+__device__ __forceinline__ c2 gl_bin(const float2* cur, const float2* prev, const float* mag,
+                                     long long base, int k, float beta, bool normalize) {
+  c2 a = cur ? mk(cur[base + k].x, cur[base + k].y) : mk(1.f, 0.f);
+  if (prev) {
+    float2 pv = prev[base + k];
+    a = a - mk(pv.x, pv.y) * beta;
+  }
+  if (normalize) {
+    float n = sqrtf(a.x * a.x + a.y * a.y) + 1e-16f;
+    a = mk(a.x / n, a.y / n);
+  }
+  if (mag) a = a * mag[base + k];
+  return a;
+}
+
+__global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict__ cur,
+                                                       const float2* __restrict__ prev,
+                                                       const float* __restrict__ mag, float beta,
+                                                       int normalize, int T, int hop,
+                                                       float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) c2 scratch[WAVES * SCR];
+  __shared__ c2 qt[QT];
+  const int b = blockIdx.y;
+  const int L = hop * (T - 1);
+  const int s0 = blockIdx.x * ISEG;  // segment start (unpadded coords)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  build_qtable(qt);
+  __syncthreads();
+  c2* S = scratch + wave * SCR;
+  // frames overlapping padded range [s0 + 1024, s0 + 1024 + ISEG)
+  const int plo = s0 + NFFT / 2, phi = s0 + NFFT / 2 + ISEG;  // [plo, phi)
+  int flo = (plo - NFFT) >= 0 ? (plo - NFFT) / hop + 1 : 0;
+  if (flo < 0) flo = 0;
+  int fhi = (phi - 1) / hop;  // frame f starts at f*hop < phi
+  if (fhi > T - 1) fhi = T - 1;
+  float acc[16], wss[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = wss[i] = 0.f;
+  const bool norm = normalize != 0;
+  for (int fb = flo; fb <= fhi; fb += WAVES) {
+    const int f = fb + wave;
+    if (f <= fhi) {
+      const long long base = ((long long)b * T + f) * NB;
+      c2 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = lane + 64 * j;
+        c2 Xk = gl_bin(cur, prev, mag, base, k, beta, norm);
+        c2 Xn = gl_bin(cur, prev, mag, base, NC - k, beta, norm);
+        if (k == 0) {
+          Xk.y = 0.f;  // irfft ignores the imaginary part of DC and Nyquist
+          Xn.y = 0.f;
+        }
+        c2 Xc = conj(Xn);
+        c2 xe = (Xk + Xc) * 0.5f;
+        c2 xo = cmul(Xk - Xc, tw<true>(qt, k)) * 0.5f;
+        v[j] = xe + mk(-xo.y, xo.x);  // Xe + i Xo
+      }
+      fft1024<true>(v, S, qt, lane);
+    }
+    __syncthreads();
+    // accumulate frames fb .. fb+7 into own samples
+    const int nf = min(WAVES, fhi - fb + 1);
+    for (int w = 0; w < nf; ++w) {
+      const int f = fb + w;
+      const float* fr = reinterpret_cast<const float*>(scratch + w * SCR);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int sp = s0 + NFFT / 2 + threadIdx.x + 512 * i;
+        const int m = sp - f * hop;
+        if (m >= 0 && m < NFFT) {
+          float wv = hann_w(qt, m);
+          acc[i] += wv * (fr[m] * (1.f / NC));
+          wss[i] += wv * wv;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* yr = y + (long long)b * L;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int s = s0 + threadIdx.x + 512 * i;
+    if (s < L) yr[s] = wss[i] > 1.17549435e-38f ? acc[i] / wss[i] : acc[i];
+  }
+}
+
+// (B, F, T) -> (B, T, F) with optional log-power -> magnitude (inference.py:109).
+__global__ void transpose_mag_kernel(const float* __restrict__ S, int F, int T, int mag_from_logpow,
+                                     float* __restrict__ St) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int f0 = blockIdx.y * 32, t0 = blockIdx.x * 32;
+  const float* Sb = S + (long long)b * F * T;
+  for (int i = threadIdx.y; i < 32; i += blockDim.y) {
+    int f = f0 + i, t = t0 + threadIdx.x;
+    float v = (f < F && t < T) ? Sb[(long long)f * T + t] : 0.f;
+    if (mag_from_logpow) v = sqrtf(expm1f(fminf(fmaxf(v, 0.f), 20.f)));
+    tile[i][threadIdx.x] = v;
+  }
+  __syncthreads();
+  float* Ob = St + (long long)b * F * T;
+  for (int i = threadIdx.y; i < 32; i += blockDim.y) {
+    int t = t0 + i, f = f0 + threadIdx.x;
+    if (f < F && t < T) Ob[(long long)t * F + f] = tile[threadIdx.x][i];
+  }
+}
+
+int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int pad_mode, float* out,
+                MelTab mel, hipStream_t st) {
+  MST_REQUIRE(x && out && B > 0 && n_fft == NFFT && hop > 0);
+  MST_REQUIRE(L > NFFT / 2 || pad_mode == MST_PAD_CONSTANT);
+  MST_REQUIRE(pad_mode == MST_PAD_REFLECT || pad_mode == MST_PAD_CONSTANT);
+  const int T = 1 + L / hop;
+  dim3 grid(ceil_div(T, FR), B), block(512);
+  switch (mode) {
+    case MODE_LOGPOW: hipLaunchKernelGGL(stft_kernel<MODE_LOGPOW>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+    case MODE_POWER: hipLaunchKernelGGL(stft_kernel<MODE_POWER>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+    case MODE_MEL: hipLaunchKernelGGL(stft_kernel<MODE_MEL>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+    default: hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+  }
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int istft_launch(const float2* cur, const float2* prev, const float* mag, float beta, int normalize,
+                 int B, int T, int hop, float* y, hipStream_t st) {
+  const int L = hop * (T - 1);
+  dim3 grid(ceil_div(L, ISEG), B), block(512);
+  hipLaunchKernelGGL(istft_kernel, grid, block, 0, st, cur, prev, mag, beta, normalize, T, hop, y);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mst_stft_logpow_f32(const float* x, int32_t B, int32_t L, int32_t n_fft, int32_t hop,
+                        int32_t pad_mode, float* out, void* stream) {
+  return stft_launch(MODE_LOGPOW, x, B, L, n_fft, hop, pad_mode, out, MelTab{}, (hipStream_t)stream);
+}
+
+int mst_stft_power_f32(const float* x, int32_t B, int32_t L, int32_t n_fft, int32_t hop,
+                       int32_t pad_mode, float* out, void* stream) {
+  return stft_launch(MODE_POWER, x, B, L, n_fft, hop, pad_mode, out, MelTab{}, (hipStream_t)stream);
+}
+
+int mst_stft_complex_f32(const float* x, int32_t B, int32_t L, int32_t n_fft, int32_t hop,
+                         int32_t pad_mode, float* out, void* stream) {
+  return stft_launch(MODE_COMPLEX, x, B, L, n_fft, hop, pad_mode, out, MelTab{}, (hipStream_t)stream);
+}
+
+int mst_stft_mel_f32(const float* x, int32_t B, int32_t L, int32_t n_fft, int32_t hop,
+                     int32_t pad_mode, const int32_t* start, const int32_t* len,
+                     const int32_t* woff, const float* w, int32_t n_mels, float* out, void* stream) {
+  MST_REQUIRE(start && len && woff && w && n_mels > 0 && n_mels <= 128);
+  MelTab mt{start, len, woff, w, n_mels};
+  return stft_launch(MODE_MEL, x, B, L, n_fft, hop, pad_mode, out, mt, (hipStream_t)stream);
+}
+
+int mst_istft_f32(const float* X, int32_t B, int32_t F, int32_t T, int32_t hop, float* y,
+                  void* stream) {
+  MST_REQUIRE(X && y && B > 0 && F == NB && T > 1 && hop > 0);
+  return istft_launch(reinterpret_cast<const float2*>(X), nullptr, nullptr, 0.f, 0, B, T, hop, y,
+                      (hipStream_t)stream);
+}
+
+size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t hop) {
+  size_t bins = (size_t)B * F * T;
+  size_t L = (size_t)hop * (T - 1);
+  // St (real) + two complex spectra + signal, each rounded to 256 B
+  auto r = [](size_t n) { return (n + 255) / 256 * 256; };
+  return r(bins * 4) + 2 * r(bins * 8) + r((size_t)B * L * 4);
+}
+
+int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
+                       float momentum, const float* angles0, int32_t mag_from_logpow, float* y,
+                       void* workspace, size_t ws_bytes, void* stream) {
+  MST_REQUIRE(S && y && workspace && B > 0 && F == NB && T > 1 && hop > 0 && n_iter >= 0);
+  MST_REQUIRE(momentum >= 0.f);
+  MST_REQUIRE(ws_bytes >= mst_griffinlim_workspace_size(B, F, T, hop));
+  MST_REQUIRE(hop * (T - 1) > NFFT / 2);
+  hipStream_t st = (hipStream_t)stream;
+  auto r = [](size_t n) { return (n + 255) / 256 * 256; };
+  size_t bins = (size_t)B * F * T;
+  char* w = (char*)workspace;
+  float* St = (float*)w;
+  float2* R0 = (float2*)(w + r(bins * 4));
+  float2* R1 = (float2*)(w + r(bins * 4) + r(bins * 8));
+  float* sig = (float*)(w + r(bins * 4) + 2 * r(bins * 8));
+  const int L = hop * (T - 1);
+  {
+    dim3 grid(ceil_div(T, 32), ceil_div(F, 32), B), block(32, 8);
+    hipLaunchKernelGGL(transpose_mag_kernel, grid, block, 0, st, S, F, T, mag_from_logpow, St);
+    MST_CHECK_LAUNCH();
+  }
+  const float beta = momentum / (1.f + momentum);
+  // iteration 0 uses the initial phases; iteration 1 has no momentum term (tprev = 0)
+  const float2* cur = reinterpret_cast<const float2*>(angles0);
+  const float2* prev = nullptr;
+  float2* bufs[2] = {R0, R1};
+  int rc;
+  for (int it = 0; it < n_iter; ++it) {
+    rc = istft_launch(cur, prev, St, beta, cur != nullptr, B, T, hop, sig, st);
+    if (rc) return rc;
+    float2* nxt = bufs[it & 1];
+    rc = stft_launch(MODE_COMPLEX, sig, B, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
+    if (rc) return rc;
+    prev = (it == 0) ? nullptr : cur;
+    cur = nxt;
+  }
+  return istft_launch(cur, prev, St, beta, cur != nullptr, B, T, hop, y, st);
+}
+
+}  // extern "C"

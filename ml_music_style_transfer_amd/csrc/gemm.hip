@@ -1,0 +1,539 @@
+// Implicit-GEMM conv/linear kernels on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// One kernel body serves every dense contraction of PerformanceNet (model/model.py):
+//   forward  Conv1d k3 p1 (model.py:14-22), Linear (model.py:98-99, NCL = 1-tap conv),
+//            ConvTranspose1d s2 p1 (model.py:24-31) as two sub-pixel phases,
+//            ConvTranspose1d k3 s1 p1 (lastconv, model.py:242)
+//   dgrad    the same layers' input gradients (stride-1 or stride-2 gathers over dY)
+//   wgrad    weight gradients: sum over (batch, time) of dY x input
+// Inputs are read through "virtual concat" descriptors (two channel slabs with time
+// offsets), which is how torch.cat + crop_and_concat (model.py:71-78, 103) are fused
+// away, and the epilogue applies alpha/bias/activation/dropout and routes rows to two
+// destinations (the concat split of an input gradient) with an optional ReLU/dropout
+// gate (DenseConcat backward).
+//
+// Tile: 128x128 block, BK=32, 256 threads = 4 waves in 2x2, each wave 64x64 = 2x2
+// MFMA 32x32 tiles. LDS holds A as [m][k] and B as [n][k] (k contiguous, row stride
+// 36 floats => conflict-free ds_read_b128 / ds_write_b128), double buffered with
+// register-staged prefetch (global loads of tile k+1 in flight during tile k's MFMAs).
+// Lane half h = lane>>5 owns k in [16h, 16h+16) of each BK tile, so one ds_read_b128
+// gives a lane four consecutive MFMA k-steps.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256, LDK = BK + 4;
+
+struct GP {
+  int M, N, K, nk, splitk;
+  // conv A operand
+  const float* A;
+  long long sAm, sAc, sAt;
+  int a_vec;
+  // wgrad A operand (P = dY or X, time contiguous)
+  const float* P;
+  long long sPb;
+  int sPc, Tk;
+  float invTk;
+  // virtual input (B operand source)
+  const float* x0;
+  long long sb0;
+  int sc0, C0, T0, off0;
+  const float* x1;
+  long long sb1;
+  int sc1, T1, off1;
+  int Tv, ta, tb, tg;
+  int Tn;
+  // conv epilogue
+  int ostride, ophase;
+  float* y0;
+  long long yb0;
+  int yc0, M0, yT0, yoff0;
+  const float* gt0;
+  float gs0;
+  float* y1;
+  long long yb1;
+  int yc1, yT1, yoff1;
+  const float* gt1;
+  float gs1;
+  float alpha;
+  const float* bias;
+  int act;
+  float drop_p;
+  unsigned long long seed;
+  // wgrad epilogue
+  float* out;
+  long long ldo;
+  float scale;
+  int accumulate;
+  // split-K slab
+  float* ws;
+};
+
+// q = k / d, r = k % d for 0 <= k < 2^24 via a float reciprocal and one correction step.
+__device__ __forceinline__ void divmod_f(int k, int d, float inv, int& q, int& r) {
+  q = (int)((float)k * inv);
+  r = k - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+}
+
+// X(b, c, tin) of the virtual concatenated input, zero outside its valid ranges.
+__device__ __forceinline__ float load_x(const GP& p, const float* base0, const float* base1, int c,
+                                        int tin) {
+  if ((unsigned)tin >= (unsigned)p.Tv) return 0.f;
+  if (c < p.C0) {
+    int ts = tin + p.off0;
+    if ((unsigned)ts >= (unsigned)p.T0) return 0.f;
+    return base0[(long long)c * p.sc0 + ts];
+  }
+  int ts = tin + p.off1;
+  if ((unsigned)ts >= (unsigned)p.T1) return 0.f;
+  return base1[(long long)(c - p.C0) * p.sc1 + ts];
+}
+
+__device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
+  if (m >= p.M || n >= p.N) return;
+  int b = n / p.Tn;
+  int t = n - b * p.Tn;
+  v *= p.alpha;
+  if (p.bias) v += p.bias[m];
+  if (p.act == MST_ACT_RELU) v = fmaxf(v, 0.f);
+  else if (p.act == MST_ACT_LRELU) v = v > 0.f ? v : 0.01f * v;
+  int to = t * p.ostride + p.ophase;
+  if (m < p.M0) {
+    int ts = to + p.yoff0;
+    if ((unsigned)ts >= (unsigned)p.yT0) return;
+    long long idx = (long long)b * p.yb0 + (long long)m * p.yc0 + ts;
+    if (p.drop_p > 0.f) {
+      uint32_t h = mst_hash32(p.seed, (unsigned long long)idx);
+      v = (h >= (uint32_t)(p.drop_p * 4294967296.0f)) ? v * (1.f / (1.f - p.drop_p)) : 0.f;
+    }
+    if (p.gt0) v = p.gt0[idx] > 0.f ? v * p.gs0 : 0.f;
+    p.y0[idx] = v;
+  } else {
+    int mm = m - p.M0;
+    int ts = to + p.yoff1;
+    if ((unsigned)ts >= (unsigned)p.yT1) return;
+    long long idx = (long long)b * p.yb1 + (long long)mm * p.yc1 + ts;
+    if (p.gt1) v = p.gt1[idx] > 0.f ? v * p.gs1 : 0.f;
+    p.y1[idx] = v;
+  }
+}
+
+__device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) {
+  if (m >= p.M || n >= p.N) return;
+  float* o = p.out + (long long)m * p.ldo + n;
+  v *= p.scale;
+  if (p.accumulate) v += *o;
+  *o = v;
+}
+
+template <int TAPS, bool WG>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int n0 = blockIdx.x * BN;
+  const int m0 = blockIdx.y * BM;
+  const int split = blockIdx.z;
+  const int kt0 = (int)((long long)split * p.nk / p.splitk);
+  const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
+
+  // ---- per-thread loader coordinates ----
+  // A tile units: rows ma = (tid>>3) + 32u (u=0..3), k quad = tid&7
+  const int akq = (tid & 7) * 4;
+  // B tile units: column nb = tid & 127, k quads (tid>>7) + 2u
+  const int nbl = tid & 127;
+  const int nb = n0 + nbl;
+  const bool nb_ok = nb < p.N;
+  const int bkq0 = (tid >> 7);
+
+  // conv B: n -> (b, t) fixed per thread
+  const float* xb0 = nullptr;
+  const float* xb1 = nullptr;
+  int tbase = 0;
+  // wgrad B: n -> (c, tap) fixed per thread
+  int wc = 0, wtap = 0;
+  if constexpr (!WG) {
+    int bb = nb_ok ? nb / p.Tn : 0;
+    int tt = nb_ok ? nb - bb * p.Tn : 0;
+    tbase = p.ta * tt + p.tb;
+    xb0 = p.x0 + (long long)bb * p.sb0;
+    xb1 = p.x1 ? p.x1 + (long long)bb * p.sb1 : nullptr;
+  } else {
+    wc = nb / TAPS;
+    wtap = nb - wc * TAPS;
+  }
+
+  float ra[4][4], rb[4][4];
+
+  auto load_tile = [&](int kt) {
+    const int k0 = kt * BK;
+    // ---------------- A ----------------
+    if constexpr (!WG) {
+      const int kk = k0 + akq;
+      if (p.a_vec) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int m = m0 + (tid >> 3) + 32 * u;
+          if (m < p.M && kk < p.K) {
+            f32x4 v = *reinterpret_cast<const f32x4*>(p.A + (long long)m * p.sAm + kk);
+            ra[u][0] = v[0]; ra[u][1] = v[1]; ra[u][2] = v[2]; ra[u][3] = v[3];
+          } else {
+            ra[u][0] = ra[u][1] = ra[u][2] = ra[u][3] = 0.f;
+          }
+        }
+      } else {
+        long long koff[4];
+        bool kok[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int k = kk + i;
+          int c = k / TAPS;
+          int tap = k - c * TAPS;
+          koff[i] = (long long)c * p.sAc + (long long)tap * p.sAt;
+          kok[i] = k < p.K;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int m = m0 + (tid >> 3) + 32 * u;
+          const float* ar = p.A + (long long)m * p.sAm;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ra[u][i] = (m < p.M && kok[i]) ? ar[koff[i]] : 0.f;
+        }
+      }
+    } else {
+      // A(m, k) = P[b][m][t], (b, t) = divmod(k, Tk)
+      const int k = k0 + akq;
+      long long off[4];
+      bool ok[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int b, t;
+        divmod_f(k + i, p.Tk, p.invTk, b, t);
+        ok[i] = (k + i) < p.K;
+        off[i] = (long long)b * p.sPb + t;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        int m = m0 + (tid >> 3) + 32 * u;
+        const float* pr = p.P + (long long)m * p.sPc;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[u][i] = (m < p.M && ok[i]) ? pr[off[i]] : 0.f;
+      }
+    }
+    // ---------------- B ----------------
+    if constexpr (!WG) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        int kq = (bkq0 + 2 * u) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int k = k0 + kq + i;
+          int c = k / TAPS;
+          int tap = k - c * TAPS;
+          float v = 0.f;
+          if (nb_ok && k < p.K) v = load_x(p, xb0, xb1, c, tbase + p.tg * tap);
+          rb[u][i] = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + (bkq0 + 2 * u) * 4;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          int b, t;
+          divmod_f(k + i, p.Tk, p.invTk, b, t);
+          float v = 0.f;
+          if (nb_ok && (k + i) < p.K) {
+            const float* base0 = p.x0 + (long long)b * p.sb0;
+            const float* base1 = p.x1 ? p.x1 + (long long)b * p.sb1 : nullptr;
+            v = load_x(p, base0, base1, wc, p.ta * t + p.tb + p.tg * wtap);
+          }
+          rb[u][i] = v;
+        }
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    float* As = lds[buf];
+    float* Bs = lds[buf] + BM * LDK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int ml = (tid >> 3) + 32 * u;
+      f32x4 v = {ra[u][0], ra[u][1], ra[u][2], ra[u][3]};
+      *reinterpret_cast<f32x4*>(As + ml * LDK + akq) = v;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      int kq = (bkq0 + 2 * u) * 4;
+      f32x4 v = {rb[u][0], rb[u][1], rb[u][2], rb[u][3]};
+      *reinterpret_cast<f32x4*>(Bs + nbl * LDK + kq) = v;
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
+      const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(As + g * 4);
+        f32x4 a1 = *reinterpret_cast<const f32x4*>(As + 32 * LDK + g * 4);
+        f32x4 b0 = *reinterpret_cast<const f32x4*>(Bs + g * 4);
+        f32x4 b1 = *reinterpret_cast<const f32x4*>(Bs + 32 * LDK + g * 4);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
+        }
+      }
+      if (more) store_tile(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores ----
+  __syncthreads();
+  float* Cs = &lds[0][0];  // 128 x 128 floats (64 KB) fits in the 72 KB of A/B buffers
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl = wn * 64 + j * 32 + r32;
+        Cs[ml * BN + nl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int nl = tid & (BN - 1);
+  const int n = n0 + nl;
+  if (n < p.N) {
+    for (int ml = tid >> 7; ml < BM; ml += NTHR / BN) {
+      const int m = m0 + ml;
+      if (m >= p.M) break;
+      const float v = Cs[ml * BN + nl];
+      if (p.splitk > 1) {
+        p.ws[((long long)split * p.M + m) * p.N + n] = v;
+      } else if constexpr (WG) {
+        wgrad_store(p, m, n, v);
+      } else {
+        conv_store(p, m, n, v);
+      }
+    }
+  }
+}
+
+template <bool WG>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GP p) {
+  long long total = (long long)p.M * p.N;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int m = (int)(i / p.N);
+    int n = (int)(i - (long long)m * p.N);
+    float v = 0.f;
+    for (int s = 0; s < p.splitk; ++s) v += p.ws[(long long)s * total + i];
+    if constexpr (WG) wgrad_store(p, m, n, v);
+    else conv_store(p, m, n, v);
+  }
+}
+
+int choose_splitk(int M, int N, int nk, int req) {
+  if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
+  long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
+  const long long target = 512;  // two workgroups per CU on 256 CUs
+  if (tiles >= 192 || nk < 8) return 1;
+  int s = (int)((target + tiles - 1) / tiles);
+  int maxs = nk / 4;  // at least four K tiles per split
+  if (s > maxs) s = maxs;
+  if (s > 32) s = 32;
+  return s < 1 ? 1 : s;
+}
+
+template <bool WG>
+int launch(const GP& p, hipStream_t st, int taps) {
+  dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
+  dim3 block(NTHR);
+#define MST_GEMM_CASE(TP) \
+  case TP: hipLaunchKernelGGL((gemm_kernel<TP, WG>), grid, block, 0, st, p); break;
+  switch (taps) {
+    MST_GEMM_CASE(1)
+    MST_GEMM_CASE(2)
+    MST_GEMM_CASE(3)
+    MST_GEMM_CASE(4)
+    MST_GEMM_CASE(6)
+    default: return MST_EINVAL;
+  }
+#undef MST_GEMM_CASE
+  MST_CHECK_LAUNCH();
+  if (p.splitk > 1) {
+    long long total = (long long)p.M * p.N;
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL((splitk_reduce_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+    MST_CHECK_LAUNCH();
+  }
+  return MST_OK;
+}
+
+bool taps_ok(int t) { return t == 1 || t == 2 || t == 3 || t == 4 || t == 6; }
+
+void fill_src(GP& p, const mst_src* s, int Ctot) {
+  p.x0 = s[0].p;
+  p.sb0 = s[0].sb;
+  p.sc0 = s[0].sc;
+  p.C0 = s[0].C;
+  p.T0 = s[0].T;
+  p.off0 = s[0].off;
+  p.x1 = s[1].C > 0 ? s[1].p : nullptr;
+  p.sb1 = s[1].sb;
+  p.sc1 = s[1].sc;
+  p.T1 = s[1].T;
+  p.off1 = s[1].off;
+  if (s[1].C <= 0) p.C0 = Ctot;  // single source covers all channels
+}
+
+int build_conv(const mst_conv_desc* d, GP& p) {
+  MST_REQUIRE(d && d->A && d->src[0].p && d->dst[0].p);
+  MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tn > 0 && d->Ctot > 0 && taps_ok(d->taps));
+  MST_REQUIRE(d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
+  MST_REQUIRE(d->dst[0].C + (d->dst[1].C > 0 ? d->dst[1].C : 0) == d->M);
+  MST_REQUIRE(d->dst[1].C <= 0 || d->dst[1].p);
+  MST_REQUIRE(d->drop_p >= 0.f && d->drop_p < 1.f);
+  p = GP{};
+  p.M = d->M;
+  p.N = d->B * d->Tn;
+  p.K = d->Ctot * d->taps;
+  p.nk = ceil_div(p.K, BK);
+  p.A = d->A;
+  p.sAm = d->sAm;
+  p.sAc = d->sAc;
+  p.sAt = d->sAt;
+  p.a_vec = (d->sAt == 1 && d->sAc == d->taps && (d->sAm % 4) == 0 && (p.K % 4) == 0 &&
+             ((uintptr_t)d->A % 16) == 0);
+  fill_src(p, d->src, d->Ctot);
+  p.Tv = d->Tv;
+  p.ta = d->a;
+  p.tb = d->beta;
+  p.tg = d->g;
+  p.Tn = d->Tn;
+  p.ostride = d->ostride;
+  p.ophase = d->ophase;
+  p.y0 = d->dst[0].p;
+  p.yb0 = d->dst[0].sb;
+  p.yc0 = d->dst[0].sc;
+  p.M0 = d->dst[0].C;
+  p.yT0 = d->dst[0].T;
+  p.yoff0 = d->dst[0].off;
+  p.gt0 = d->dst[0].gate;
+  p.gs0 = d->dst[0].gate_scale;
+  p.y1 = d->dst[1].C > 0 ? d->dst[1].p : nullptr;
+  p.yb1 = d->dst[1].sb;
+  p.yc1 = d->dst[1].sc;
+  p.yT1 = d->dst[1].T;
+  p.yoff1 = d->dst[1].off;
+  p.gt1 = d->dst[1].gate;
+  p.gs1 = d->dst[1].gate_scale;
+  p.alpha = d->alpha;
+  p.bias = d->bias;
+  p.act = d->act;
+  p.drop_p = d->drop_p;
+  p.seed = d->seed;
+  p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
+  return MST_OK;
+}
+
+int build_wgrad(const mst_wgrad_desc* d, GP& p) {
+  MST_REQUIRE(d && d->P && d->src[0].p && d->out);
+  MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tk > 0 && d->Ctot > 0 && taps_ok(d->taps));
+  MST_REQUIRE(d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
+  p = GP{};
+  p.M = d->M;
+  p.N = d->Ctot * d->taps;
+  p.K = d->B * d->Tk;
+  p.nk = ceil_div(p.K, BK);
+  p.P = d->P;
+  p.sPb = d->sPb;
+  p.sPc = d->sPc;
+  p.Tk = d->Tk;
+  p.invTk = 1.0f / (float)d->Tk;
+  fill_src(p, d->src, d->Ctot);
+  p.Tv = d->Tv;
+  p.ta = d->a;
+  p.tb = d->beta;
+  p.tg = d->g;
+  p.out = d->out;
+  p.ldo = d->ldo;
+  p.scale = d->scale;
+  p.accumulate = d->accumulate;
+  p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
+  return MST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mst_conv_fwd_workspace_size(const mst_conv_desc* d) {
+  GP p;
+  if (build_conv(d, p) != MST_OK) return 0;
+  return p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+}
+
+int mst_conv_fwd_f32(const mst_conv_desc* d, float* ws, size_t ws_bytes, void* stream) {
+  GP p;
+  int rc = build_conv(d, p);
+  if (rc) return rc;
+  if (p.splitk > 1) {
+    size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
+    if (!ws || ws_bytes < need) p.splitk = 1;  // fall back to a single K pass
+    p.ws = ws;
+  }
+  return launch<false>(p, (hipStream_t)stream, d->taps);
+}
+
+size_t mst_wgrad_workspace_size(const mst_wgrad_desc* d) {
+  GP p;
+  if (build_wgrad(d, p) != MST_OK) return 0;
+  return p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+}
+
+int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* ws, size_t ws_bytes, void* stream) {
+  GP p;
+  int rc = build_wgrad(d, p);
+  if (rc) return rc;
+  if (p.splitk > 1) {
+    size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
+    if (!ws || ws_bytes < need) p.splitk = 1;
+    p.ws = ws;
+  }
+  return launch<true>(p, (hipStream_t)stream, d->taps);
+}
+
+}  // extern "C"

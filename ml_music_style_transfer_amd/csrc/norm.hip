@@ -1,0 +1,560 @@
+// Bandwidth-bound kernels of the training step (one wave per NCL row where a row reduction
+// is needed):
+//   InstanceNorm1d(eps=1e-5, no affine) + LeakyReLU(0.01) [+ MaxPool1d(2,2)] fwd/bwd
+//       model/model.py:40-53 (DownConv), 65-69 + 81-89 (UpConv)
+//   bias gradients (sum over batch and time)
+//   lrelu(lastconv) + L1 loss fwd/bwd   model/model.py:299, model/train.py:132-135,140
+//   Adam over the flat parameter buffer  model/train.py:188,143
+//   piano-roll binarise + onset/offset   preprocessing/preprocess.py:148-155
+#include "common.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// InstanceNorm + LeakyReLU (+ MaxPool) forward. One wave per row; lane l holds the
+// element pairs (2l + 128p, 2l + 128p + 1), p < NP, so the pool pairs are lane-local.
+// Two-pass (exact) mean/variance in registers; biased variance like torch.
+// ---------------------------------------------------------------------------
+template <int NP>
+__global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y, long long rows,
+                                                     int T, float eps, float slope,
+                                                     float* __restrict__ a, float* __restrict__ pooled,
+                                                     float* __restrict__ mean,
+                                                     float* __restrict__ rstd) {
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + row * T;
+  float e0[NP], e1[NP];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    int i0 = 2 * lane + 128 * q;
+    e0[q] = i0 < T ? yr[i0] : 0.f;
+    e1[q] = i0 + 1 < T ? yr[i0 + 1] : 0.f;
+    s += e0[q] + e1[q];
+  }
+  s = wave_sum(s);
+  const float mu = s / (float)T;
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    int i0 = 2 * lane + 128 * q;
+    float d0 = e0[q] - mu, d1 = e1[q] - mu;
+    if (i0 < T) v += d0 * d0;
+    if (i0 + 1 < T) v += d1 * d1;
+  }
+  v = wave_sum(v);
+  const float r = 1.f / sqrtf(v / (float)T + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = r;
+  }
+  float* ar = a + row * T;
+  const int Tp = T >> 1;
+  float* pr = pooled ? pooled + row * Tp : nullptr;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    int i0 = 2 * lane + 128 * q;
+    float a0 = lrelu((e0[q] - mu) * r, slope);
+    float a1 = lrelu((e1[q] - mu) * r, slope);
+    if (i0 < T) ar[i0] = a0;
+    if (i0 + 1 < T) ar[i0 + 1] = a1;
+    if (pr && (i0 >> 1) < Tp) pr[i0 >> 1] = (a1 > a0) ? a1 : a0;  // first index wins ties
+  }
+}
+
+// Long rows (T > 128*16): three streaming passes over global memory.
+__global__ __launch_bounds__(256) void in_fwd_long_kernel(const float* __restrict__ y,
+                                                          long long rows, int T, float eps,
+                                                          float slope, float* __restrict__ a,
+                                                          float* __restrict__ pooled,
+                                                          float* __restrict__ mean,
+                                                          float* __restrict__ rstd) {
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + row * T;
+  float s = 0.f;
+  for (int i = lane; i < T; i += 64) s += yr[i];
+  const float mu = wave_sum(s) / (float)T;
+  float v = 0.f;
+  for (int i = lane; i < T; i += 64) {
+    float d = yr[i] - mu;
+    v += d * d;
+  }
+  const float r = 1.f / sqrtf(wave_sum(v) / (float)T + eps);
+  if (lane == 0) {
+    mean[row] = mu;
+    rstd[row] = r;
+  }
+  float* ar = a + row * T;
+  const int Tp = T >> 1;
+  for (int i0 = 2 * lane; i0 < T; i0 += 128) {
+    float a0 = lrelu((yr[i0] - mu) * r, slope);
+    ar[i0] = a0;
+    if (i0 + 1 < T) {
+      float a1 = lrelu((yr[i0 + 1] - mu) * r, slope);
+      ar[i0 + 1] = a1;
+      if (pooled && (i0 >> 1) < Tp) pooled[row * Tp + (i0 >> 1)] = (a1 > a0) ? a1 : a0;
+    }
+  }
+}
+
+// Backward: da = d_a + unpool(d_pool0 + d_pool1) (to the pair's argmax), dz = lrelu'(z) da,
+// dy = rstd * (dz - mean(dz) - z * mean(dz * z)).
+template <int NP>
+__global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd,
+                                                     long long rows, int T, float slope,
+                                                     const float* __restrict__ d_a,
+                                                     const float* __restrict__ dp0,
+                                                     const float* __restrict__ dp1,
+                                                     float* __restrict__ dy) {
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + row * T;
+  const float mu = mean[row], r = rstd[row];
+  const int Tp = T >> 1;
+  float z0[NP], z1[NP], g0[NP], g1[NP];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    int i0 = 2 * lane + 128 * q;
+    bool ok0 = i0 < T, ok1 = i0 + 1 < T;
+    float y0 = ok0 ? yr[i0] : mu, y1 = ok1 ? yr[i0 + 1] : mu;
+    z0[q] = (y0 - mu) * r;
+    z1[q] = (y1 - mu) * r;
+    float da0 = 0.f, da1 = 0.f;
+    if (d_a) {
+      if (ok0) da0 = d_a[row * T + i0];
+      if (ok1) da1 = d_a[row * T + i0 + 1];
+    }
+    int pi = i0 >> 1;
+    if ((dp0 || dp1) && pi < Tp) {
+      float gp = (dp0 ? dp0[row * Tp + pi] : 0.f) + (dp1 ? dp1[row * Tp + pi] : 0.f);
+      float a0 = lrelu(z0[q], slope), a1 = lrelu(z1[q], slope);
+      if (a1 > a0) da1 += gp;
+      else da0 += gp;
+    }
+    g0[q] = ok0 ? (z0[q] > 0.f ? da0 : da0 * slope) : 0.f;
+    g1[q] = ok1 ? (z1[q] > 0.f ? da1 : da1 * slope) : 0.f;
+    s1 += g0[q] + g1[q];
+    s2 += g0[q] * z0[q] + g1[q] * z1[q];
+  }
+  s1 = wave_sum(s1) / (float)T;
+  s2 = wave_sum(s2) / (float)T;
+  float* dr = dy + row * T;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    int i0 = 2 * lane + 128 * q;
+    if (i0 < T) dr[i0] = r * (g0[q] - s1 - z0[q] * s2);
+    if (i0 + 1 < T) dr[i0 + 1] = r * (g1[q] - s1 - z1[q] * s2);
+  }
+}
+
+__device__ __forceinline__ float in_bwd_g(const float* yr, int i, int T, int Tp, float mu, float r,
+                                          float slope, const float* da_r, const float* dp0r,
+                                          const float* dp1r, float* zout) {
+  float z = (yr[i] - mu) * r;
+  *zout = z;
+  float da = da_r ? da_r[i] : 0.f;
+  int pi = i >> 1;
+  if ((dp0r || dp1r) && pi < Tp) {
+    int j = i ^ 1;
+    float zo = (yr[j] - mu) * r;
+    float a = lrelu(z, slope), ao = lrelu(zo, slope);
+    bool second_wins = (i & 1) ? (a > ao) : (ao > a);
+    bool mine = (i & 1) ? second_wins : !second_wins;
+    if (mine) da += (dp0r ? dp0r[pi] : 0.f) + (dp1r ? dp1r[pi] : 0.f);
+  }
+  return z > 0.f ? da : da * slope;
+}
+
+__global__ __launch_bounds__(256) void in_bwd_long_kernel(const float* __restrict__ y,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          long long rows, int T, float slope,
+                                                          const float* __restrict__ d_a,
+                                                          const float* __restrict__ dp0,
+                                                          const float* __restrict__ dp1,
+                                                          float* __restrict__ dy) {
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* yr = y + row * T;
+  const float mu = mean[row], r = rstd[row];
+  const int Tp = T >> 1;
+  const float* dar = d_a ? d_a + row * T : nullptr;
+  const float* p0 = dp0 ? dp0 + row * Tp : nullptr;
+  const float* p1 = dp1 ? dp1 + row * Tp : nullptr;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = lane; i < T; i += 64) {
+    float z;
+    float g = in_bwd_g(yr, i, T, Tp, mu, r, slope, dar, p0, p1, &z);
+    s1 += g;
+    s2 += g * z;
+  }
+  s1 = wave_sum(s1) / (float)T;
+  s2 = wave_sum(s2) / (float)T;
+  for (int i = lane; i < T; i += 64) {
+    float z;
+    float g = in_bwd_g(yr, i, T, Tp, mu, r, slope, dar, p0, p1, &z);
+    dy[row * T + i] = r * (g - s1 - z * s2);
+  }
+}
+
+// db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one block per channel.
+__global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dy, int B, int C,
+                                                        int T, float scale, float* __restrict__ db,
+                                                        int accumulate) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* r = dy + ((long long)b * C + c) * T;
+    for (int t = threadIdx.x; t < T; t += blockDim.x) s += r[t];
+  }
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = (red[0] + red[1] + red[2] + red[3]) * scale;
+    if (accumulate) v += db[c];
+    db[c] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// L1 / MSE loss: per-block double partials, then one block finishes (deterministic).
+// ---------------------------------------------------------------------------
+template <int MODE>  // 0: L1 of lrelu(pre) vs t (writes y), 1: L1(pred, t), 2: MSE(pred, t)
+__global__ __launch_bounds__(256) void loss_partial_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ t,
+                                                           long long n, float slope,
+                                                           float* __restrict__ y,
+                                                           double* __restrict__ part) {
+  double s = 0.0;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = x[i];
+    if (MODE == 0) {
+      v = lrelu(v, slope);
+      if (y) y[i] = v;
+    }
+    float d = v - t[i];
+    s += (MODE == 2) ? (double)d * d : (double)fabsf(d);
+  }
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void loss_final_kernel(const double* __restrict__ part, int nb,
+                                                         long long n, float* __restrict__ loss) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) loss[0] = (float)((red[0] + red[1] + red[2] + red[3]) / (double)n);
+}
+
+__global__ __launch_bounds__(256) void l1_lrelu_bwd_kernel(const float* __restrict__ pre,
+                                                           const float* __restrict__ t, long long n,
+                                                           float slope,
+                                                           const float* __restrict__ gscale,
+                                                           float* __restrict__ dpre) {
+  const float g = (gscale ? gscale[0] : 1.f) / (float)n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float p = pre[i];
+    float d = lrelu(p, slope) - t[i];
+    float sg = d > 0.f ? g : (d < 0.f ? -g : 0.f);
+    dpre[i] = p > 0.f ? sg : sg * slope;
+  }
+}
+
+// Adam (torch.optim.Adam, single-tensor formulation): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g^2;
+// p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps). Vectorised 4-wide over the flat buffer.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   long long n, float lr_step, float b1, float b2,
+                                                   float eps, float bc2_sqrt) {
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
+  long long n4 = n >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    f32x4 mv = reinterpret_cast<f32x4*>(m)[i];
+    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mv[k] = mv[k] + w1 * (gv[k] - mv[k]);
+      vv[k] = vv[k] * b2 + w2 * (gv[k] * gv[k]);
+      float den = sqrtf(vv[k]) / bc2_sqrt + eps;
+      pv[k] = pv[k] - lr_step * (mv[k] / den);
+    }
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    reinterpret_cast<f32x4*>(m)[i] = mv;
+    reinterpret_cast<f32x4*>(v)[i] = vv;
+  }
+  // tail
+  long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && i < n) {
+    float gv = g[i], mv = m[i], vv = v[i];
+    mv = mv + w1 * (gv - mv);
+    vv = vv * b2 + w2 * (gv * gv);
+    float den = sqrtf(vv) / bc2_sqrt + eps;
+    p[i] = p[i] - lr_step * (mv / den);
+    m[i] = mv;
+    v[i] = vv;
+  }
+}
+
+__global__ void scale_kernel(float* x, long long n, float s) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    x[i] *= s;
+}
+
+__global__ void fill_kernel(float* x, long long n, float v) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    x[i] = v;
+}
+
+// preprocess.py:148-155: bin = roll != 0; onoff[t] = bin[t] - bin[t-1] (bin[-1] = 0).
+__global__ void onoff_kernel(const float* __restrict__ roll, int B, int T, float* __restrict__ bin,
+                             float* __restrict__ onoff) {
+  long long n = (long long)B * T * 128;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    int t = (int)((i / 128) % T);
+    float cur = roll[i] != 0.f ? 1.f : 0.f;
+    float prev = (t > 0 && roll[i - 128] != 0.f) ? 1.f : 0.f;
+    bin[i] = cur;
+    onoff[i] = cur - prev;
+  }
+}
+
+// dx = gscale[0]/n * sign(pred - t)   (nn.L1Loss backward; sign(0) = 0)
+__global__ void l1_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ t,
+                              long long n, const float* __restrict__ gscale, float* __restrict__ dx) {
+  const float g = (gscale ? gscale[0] : 1.f) / (float)n;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float d = pred[i] - t[i];
+    dx[i] = d > 0.f ? g : (d < 0.f ? -g : 0.f);
+  }
+}
+
+// dx = dy * (y > 0 ? 1 : slope)   (LeakyReLU backward from its output's sign)
+__global__ void lrelu_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                 long long n, float slope, float* __restrict__ dx) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float g = dy[i];
+    dx[i] = y[i] > 0.f ? g : g * slope;
+  }
+}
+
+// out = h > 0 ? d * s : 0   (ReLU + inverted-dropout backward from the kept output h)
+__global__ void relu_gate_bwd_kernel(const float* __restrict__ d, const float* __restrict__ h,
+                                     long long n, float s, float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = h[i] > 0.f ? d[i] * s : 0.f;
+}
+
+// y = a * x + b * y
+__global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, long long n,
+                             float a, float b) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    y[i] = a * x[i] + b * y[i];
+}
+
+int grid_for(long long n, int per = 256, int cap = 8192) {
+  long long g = (n + per - 1) / per;
+  if (g > cap) g = cap;
+  return g < 1 ? 1 : (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mst_instnorm_lrelu_fwd_f32(const float* y, int64_t rows, int32_t T, float eps, float slope,
+                               float* a, float* pooled, float* mean, float* rstd, void* stream) {
+  MST_REQUIRE(y && a && mean && rstd && rows > 0 && T > 1);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  int np = (T + 127) / 128;
+  if (np <= 1) hipLaunchKernelGGL(in_fwd_kernel<1>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  else if (np <= 2) hipLaunchKernelGGL(in_fwd_kernel<2>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  else if (np <= 4) hipLaunchKernelGGL(in_fwd_kernel<4>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  else if (np <= 8) hipLaunchKernelGGL(in_fwd_kernel<8>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  else hipLaunchKernelGGL(in_fwd_long_kernel, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* rstd, int64_t rows,
+                               int32_t T, float slope, const float* d_a, const float* d_pool0,
+                               const float* d_pool1, float* dy, void* stream) {
+  MST_REQUIRE(y && mean && rstd && dy && rows > 0 && T > 1);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  int np = (T + 127) / 128;
+  if (np <= 1) hipLaunchKernelGGL(in_bwd_kernel<1>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  else if (np <= 2) hipLaunchKernelGGL(in_bwd_kernel<2>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  else if (np <= 4) hipLaunchKernelGGL(in_bwd_kernel<4>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  else if (np <= 8) hipLaunchKernelGGL(in_bwd_kernel<8>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  else hipLaunchKernelGGL(in_bwd_long_kernel, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float scale, float* db,
+                      int32_t accumulate, void* stream) {
+  MST_REQUIRE(dy && db && B > 0 && C > 0 && T > 0);
+  hipLaunchKernelGGL(bias_grad_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, B, C, T,
+                     scale, db, accumulate);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+size_t mst_l1_workspace_size(int64_t n) { return (size_t)grid_for(n, 256 * 8, 1024) * sizeof(double); }
+
+static int loss_launch(int mode, const float* x, const float* t, int64_t n, float slope, float* y,
+                       float* loss, void* ws, void* stream) {
+  MST_REQUIRE(x && t && loss && ws && n > 0);
+  hipStream_t st = (hipStream_t)stream;
+  int nb = grid_for(n, 256 * 8, 1024);
+  double* part = (double*)ws;
+  if (mode == 0) hipLaunchKernelGGL(loss_partial_kernel<0>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
+  else if (mode == 1) hipLaunchKernelGGL(loss_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
+  else hipLaunchKernelGGL(loss_partial_kernel<2>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
+  MST_CHECK_LAUNCH();
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part, nb, (long long)n, loss);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_l1_lrelu_fwd_f32(const float* ypre, const float* target, int64_t n, float slope, float* y,
+                         float* loss, void* ws, void* stream) {
+  return loss_launch(0, ypre, target, n, slope, y, loss, ws, stream);
+}
+int mst_l1_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* ws,
+                   void* stream) {
+  return loss_launch(1, pred, target, n, 0.f, nullptr, loss, ws, stream);
+}
+int mst_mse_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* ws,
+                    void* stream) {
+  return loss_launch(2, pred, target, n, 0.f, nullptr, loss, ws, stream);
+}
+
+int mst_l1_lrelu_bwd_f32(const float* ypre, const float* target, int64_t n, float slope,
+                         const float* gscale, float* dypre, void* stream) {
+  MST_REQUIRE(ypre && target && dypre && n > 0);
+  hipLaunchKernelGGL(l1_lrelu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
+                     ypre, target, (long long)n, slope, gscale, dypre);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_l1_bwd_f32(const float* pred, const float* target, int64_t n, const float* gscale, float* dx,
+                   void* stream) {
+  MST_REQUIRE(pred && target && dx && n > 0);
+  hipLaunchKernelGGL(l1_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, pred,
+                     target, (long long)n, gscale, dx);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_lrelu_bwd_f32(const float* dy, const float* y, int64_t n, float slope, float* dx,
+                      void* stream) {
+  MST_REQUIRE(dy && y && dx && n > 0);
+  hipLaunchKernelGGL(lrelu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, y,
+                     (long long)n, slope, dx);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, float* out,
+                          void* stream) {
+  MST_REQUIRE(d && h && out && n > 0);
+  hipLaunchKernelGGL(relu_gate_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d,
+                     h, (long long)n, s, out);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_axpby_f32(const float* x, float* y, int64_t n, float a, float b, void* stream) {
+  MST_REQUIRE(x && y && n >= 0);
+  if (n == 0) return MST_OK;
+  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y,
+                     (long long)n, a, b);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
+                 float b2, float eps, float bc2_sqrt, void* stream) {
+  MST_REQUIRE(p && g && m && v && n > 0);
+  MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b1, b2, eps, bc2_sqrt);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_scale_f32(float* x, int64_t n, float s, void* stream) {
+  MST_REQUIRE(x && n >= 0);
+  if (n == 0) return MST_OK;
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)n, s);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_fill_f32(float* x, int64_t n, float v, void* stream) {
+  MST_REQUIRE(x && n >= 0);
+  if (n == 0) return MST_OK;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x,
+                     (long long)n, v);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_onoff_f32(const float* roll, int32_t B, int32_t T, float* bin, float* onoff, void* stream) {
+  MST_REQUIRE(roll && bin && onoff && B > 0 && T > 0);
+  hipLaunchKernelGGL(onoff_kernel, dim3(grid_for((long long)B * T * 128)), dim3(256), 0,
+                     (hipStream_t)stream, roll, B, T, bin, onoff);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+const char* mst_version(void) { return "libmst_hip 0.1 gfx950"; }
+
+int mst_device_arch(char* buf, int32_t n) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return -(int)e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, dev);
+  if (e != hipSuccess) return -(int)e;
+  int i = 0;
+  for (; i + 1 < n && prop.gcnArchName[i]; ++i) buf[i] = prop.gcnArchName[i];
+  if (n > 0) buf[i] = 0;
+  return MST_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,370 @@
+"""Forward/backward programs of PerformanceNet on libmst_hip.
+
+Each reference block (model/model.py) is a pair of functions operating on raw
+device tensors: `*_fwd` enqueues the block's kernels and returns its outputs
+plus a saved-state tuple; `*_bwd` enqueues the backward kernels, writes weight
+gradients straight into each parameter's `.grad` (a view of the model's flat
+gradient buffer) and returns input gradients. The whole network forward is ONE
+autograd node (`PerformanceNetFunction`), so backward runs this hand-scheduled
+program instead of ~200 generic autograd nodes, and cross-block fusions are
+possible:
+
+  * torch.cat / crop_and_concat (model.py:71-78, 103) never materialise: GEMM
+    loaders read two sources with time offsets, and dgrad epilogues split the
+    concatenated input gradient back into its parts;
+  * the maxpool gradient and the skip gradient of an encoder level are summed
+    inside the InstanceNorm backward kernel (no accumulation pass);
+  * MBRBlock x4 returns 16*x exactly (model.py:172 discards its residual sum),
+    so its dead convolutions are skipped and the 16 folds into lastconv's GEMM
+    (alpha) — output- and gradient-identical to the reference;
+  * lastconv's LeakyReLU runs in the GEMM epilogue; DenseConcat's
+    ReLU+Dropout backward is applied by the fc2-dgrad epilogue as a gate.
+
+Gradient accumulation follows torch semantics: a parameter whose .grad is None
+gets a fresh gradient (written, not added); otherwise the kernel adds into it.
+"""
+import torch
+
+from . import _lib as L
+from . import kernels as K
+
+LRELU = L.ACT_LRELU
+RELU = L.ACT_RELU
+
+
+def _e(shape, like):
+    return torch.empty(shape, device=like.device, dtype=torch.float32)
+
+
+class GradSink:
+    """Where weight gradients go: p.grad if present (accumulate) else a fresh buffer."""
+
+    def __init__(self, flat_grad_of=None):
+        self.flat_grad_of = flat_grad_of or (lambda p: None)
+
+    def target(self, p):
+        if p.grad is None:
+            g = self.flat_grad_of(p)
+            if g is None:
+                g = torch.empty_like(p)
+            p.grad = g
+            return g, False
+        return p.grad, True
+
+
+# ------------------------------------------------------------------ DownConv
+def downconv_fwd(W1, b1, W2, b2, x, pool):
+    """DownConv.forward (model.py:47-53). Returns (out, before_pool, saved)."""
+    B, _, T = x.shape
+    Cout = W1.shape[0]
+    y1 = _e((B, Cout, T), x)
+    K.conv3_fwd([(x, 0)], W1, b1, y1)
+    a1, _, m1, r1 = K.in_lrelu_fwd(y1, False)
+    y2 = _e((B, Cout, T), x)
+    K.conv3_fwd([(a1, 0)], W2, b2, y2)
+    a2, pooled, m2, r2 = K.in_lrelu_fwd(y2, pool)
+    saved = (x, y1, m1, r1, a1, y2, m2, r2)
+    return (pooled if pool else a2), a2, saved
+
+
+def downconv_bwd(params, saved, sink, d_before=None, d_pool0=None, d_pool1=None, need_dx=True):
+    W1, b1, W2, b2 = params
+    x, y1, m1, r1, a1, y2, m2, r2 = saved
+    dy2 = K.in_lrelu_bwd(y2, m2, r2, d_before, d_pool0, d_pool1)
+    g, acc = sink.target(W2)
+    K.conv3_wgrad(dy2, [(a1, 0)], g, acc)
+    g, acc = sink.target(b2)
+    K.bias_grad(dy2, g, acc)
+    da1 = torch.empty_like(a1)
+    K.conv3_dgrad(dy2, W2, [(da1, 0, None, 1.0)])
+    del dy2
+    dy1 = K.in_lrelu_bwd(y1, m1, r1, da1)
+    del da1
+    g, acc = sink.target(W1)
+    K.conv3_wgrad(dy1, [(x, 0)], g, acc)
+    g, acc = sink.target(b1)
+    K.bias_grad(dy1, g, acc)
+    if not need_dx:
+        return None
+    dx = torch.empty_like(x)
+    K.conv3_dgrad(dy1, W1, [(dx, 0, None, 1.0)])
+    return dx
+
+
+# ---------------------------------------------------------------- DenseConcat
+def dense_fwd(W1, b1, W2, b2, midi, audio, drop_p=0.0, seed=0):
+    """DenseConcat.forward (model.py:102-108): cat(audio, midi) -> fc1 -> ReLU -> Dropout
+    -> fc2 -> ReLU -> Dropout, computed in NCL (no transposes)."""
+    B, _, T = midi.shape
+    h1 = _e((B, W1.shape[0], T), midi)
+    K.linear_fwd([(audio, 0), (midi, 0)], W1, b1, h1, act=RELU, drop_p=drop_p, seed=seed)
+    h2 = _e((B, W2.shape[0], T), midi)
+    K.linear_fwd([(h1, 0)], W2, b2, h2, act=RELU, drop_p=drop_p, seed=seed + 1)
+    return h2, (midi, audio, h1, h2, drop_p)
+
+
+def dense_bwd(params, saved, sink, d_h2, need_dx=True, gated=False):
+    """gated=True: d_h2 already is d(fc2 pre-activation) (gate applied by the producer)."""
+    W1, b1, W2, b2 = params
+    midi, audio, h1, h2, drop_p = saved
+    s = 1.0 / (1.0 - drop_p)
+    dpre2 = d_h2 if gated else K.relu_gate_bwd(d_h2, h2, s)
+    g, acc = sink.target(W2)
+    K.linear_wgrad(dpre2, [(h1, 0)], g, acc)
+    g, acc = sink.target(b2)
+    K.bias_grad(dpre2, g, acc)
+    dpre1 = torch.empty_like(h1)
+    K.linear_dgrad(dpre2, W2, [(dpre1, 0, h1, s)])
+    del dpre2
+    g, acc = sink.target(W1)
+    K.linear_wgrad(dpre1, [(audio, 0), (midi, 0)], g, acc)
+    g, acc = sink.target(b1)
+    K.bias_grad(dpre1, g, acc)
+    if not need_dx:
+        return None, None
+    d_audio = torch.empty_like(audio)
+    d_midi = torch.empty_like(midi)
+    K.linear_dgrad(dpre1, W1, [(d_audio, 0, None, 1.0), (d_midi, 0, None, 1.0)])
+    return d_midi, d_audio
+
+
+# --------------------------------------------------------------------- UpConv
+def crop_offset(L_bypass, L_up):
+    """crop_and_concat (model.py:71-77) == bypass shifted by c = (Lb - Lu)//2."""
+    return (L_bypass - L_up) // 2
+
+
+def upconv_fwd(Wu, bu, W1, b1, W2, b2, res, dec, cond):
+    """UpConv.forward (model.py:80-90)."""
+    B, _, Tin = dec.shape
+    k = Wu.shape[2]
+    Co = Wu.shape[1]
+    Lu = K.convT2_out_len(Tin, k)
+    u_pre = _e((B, Co, Lu), dec)
+    K.convT2_fwd(dec, Wu, bu, u_pre)
+    u, _, mu_, ru_ = K.in_lrelu_fwd(u_pre, False)
+    c_res = crop_offset(res.shape[2], Lu)
+    v_pre = _e((B, Co, Lu), dec)
+    K.conv3_fwd([(u, 0), (res, c_res)], W1, b1, v_pre)
+    v, _, mv_, rv_ = K.in_lrelu_fwd(v_pre, False)
+    srcs2 = [(v, 0)]
+    c_cond = 0
+    if cond is not None:
+        c_cond = crop_offset(cond.shape[2], Lu)
+        srcs2.append((cond, c_cond))
+    w_pre = _e((B, Co, Lu), dec)
+    K.conv3_fwd(srcs2, W2, b2, w_pre)
+    w, _, mw_, rw_ = K.in_lrelu_fwd(w_pre, False)
+    saved = (dec, u_pre, mu_, ru_, u, res, c_res, v_pre, mv_, rv_, v, cond, c_cond, w_pre, mw_, rw_)
+    return w, saved
+
+
+def _grad_buffer_for_bypass(t, c, Lu):
+    """Gradient buffer of a crop_and_concat bypass: positions s with s - c outside [0, Lu)
+    never reach the output and must read zero (only when the crop trims the bypass)."""
+    covered = c <= 0 and t.shape[2] - c <= Lu
+    return torch.empty_like(t) if covered else torch.zeros_like(t)
+
+
+def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_gate=None,
+               dec_gate_scale=1.0):
+    """Returns (d_res, d_dec, d_cond). res_gate/dec_gate apply a producer DenseConcat's
+    ReLU/dropout backward inside the dgrad epilogues (the result is d(fc2 pre-activation))."""
+    Wu, bu, W1, b1, W2, b2 = params
+    (dec, u_pre, mu_, ru_, u, res, c_res, v_pre, mv_, rv_, v, cond, c_cond, w_pre, mw_,
+     rw_) = saved
+    dw_pre = K.in_lrelu_bwd(w_pre, mw_, rw_, d_w)
+    srcs2 = [(v, 0)] + ([(cond, c_cond)] if cond is not None else [])
+    g, acc = sink.target(W2)
+    K.conv3_wgrad(dw_pre, srcs2, g, acc)
+    g, acc = sink.target(b2)
+    K.bias_grad(dw_pre, g, acc)
+    dv = torch.empty_like(v)
+    dsts = [(dv, 0, None, 1.0)]
+    d_cond = None
+    if cond is not None:
+        d_cond = _grad_buffer_for_bypass(cond, c_cond, v.shape[2])
+        dsts.append((d_cond, c_cond, None, 1.0))
+    K.conv3_dgrad(dw_pre, W2, dsts)
+    del dw_pre
+    dv_pre = K.in_lrelu_bwd(v_pre, mv_, rv_, dv)
+    del dv
+    g, acc = sink.target(W1)
+    K.conv3_wgrad(dv_pre, [(u, 0), (res, c_res)], g, acc)
+    g, acc = sink.target(b1)
+    K.bias_grad(dv_pre, g, acc)
+    du = torch.empty_like(u)
+    d_res = _grad_buffer_for_bypass(res, c_res, u.shape[2])
+    K.conv3_dgrad(dv_pre, W1, [(du, 0, None, 1.0), (d_res, c_res, res_gate, res_gate_scale)])
+    del dv_pre
+    du_pre = K.in_lrelu_bwd(u_pre, mu_, ru_, du)
+    del du
+    g, acc = sink.target(Wu)
+    K.convT2_wgrad(dec, du_pre, g, acc)
+    g, acc = sink.target(bu)
+    K.bias_grad(du_pre, g, acc)
+    d_dec = torch.empty_like(dec)
+    K.convT2_dgrad(du_pre, Wu, [(d_dec, 0, dec_gate, dec_gate_scale)])
+    return d_res, d_dec, d_cond
+
+
+# ----------------------------------------------------------- whole network
+MBR_SCALE = 16.0  # 4 MBRBlocks x (returns 2*x), model.py:172-173,295-298
+
+
+def _pp(P, prefix, names):
+    return tuple(P[f"{prefix}.{n}"] for n in names)
+
+
+DC = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")
+DN = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
+UP = ("upconv.weight", "upconv.bias", "conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")
+
+
+def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5):
+    """PerformanceNet.forward (model.py:262-300) as one kernel program."""
+    enc_m, enc_a, sv_m, sv_a = [], [], [], []
+    xm = x_midi
+    for i in range(depth):
+        xm, before, sv = downconv_fwd(*_pp(P, f"down_convs.{i}", DC), xm, i < depth - 1)
+        enc_m.append(before)
+        sv_m.append(sv)
+    xa = x_audio
+    for i in range(depth):
+        xa, before, sv = downconv_fwd(*_pp(P, f"down_convs_audio.{i}", DC), xa, i < depth - 1)
+        enc_a.append(before)
+        sv_a.append(sv)
+    x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed)
+    conds, sv_o = [], []
+    c = cond
+    for i in range(3):
+        c, _, sv = downconv_fwd(*_pp(P, f"onset_offset_encoder.down_convs.{i}", DC), c, True)
+        sv_o.append(sv)
+        if i > 0:
+            conds.append(c)
+    sv_dn, sv_up = [], []
+    for i in range(4):
+        skip, svd = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
+                              enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1))
+        cd = conds[i - 1] if i < 2 else None
+        x, svu = upconv_fwd(*_pp(P, f"up_convs.{i}", UP), skip, x, cd)
+        sv_dn.append(svd)
+        sv_up.append(svu)
+    W, b = P["lastconv.weight"], P["lastconv.bias"]
+    B, _, T = x.shape
+    y = _e((B, W.shape[1], T), x)
+    K.convT1_fwd(x, W, b, y, alpha=MBR_SCALE, act=LRELU)
+    state = dict(sv_m=sv_m, sv_a=sv_a, sv_d0=sv_d0, sv_o=sv_o, sv_dn=sv_dn, sv_up=sv_up, x_dec=x,
+                 y=y, depth=depth)
+    return y, state
+
+
+def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
+    depth = st["depth"]
+    y = st["y"]
+    dypre = K.lrelu_bwd(dy, y)
+    W = P["lastconv.weight"]
+    x_dec = st["x_dec"]
+    g, acc = sink.target(W)
+    K.convT1_wgrad(x_dec, dypre, g, acc, scale=MBR_SCALE)
+    g, acc = sink.target(P["lastconv.bias"])
+    K.bias_grad(dypre, g, acc)
+    dx = torch.empty_like(x_dec)
+    K.convT1_dgrad(dypre, W, dx, alpha=MBR_SCALE)
+    del dypre
+    d_before_m = [None] * depth
+    d_before_a = [None] * depth
+    d_conds = [None, None]
+    sv_d0 = st["sv_d0"]
+    for i in reversed(range(4)):
+        svd = st["sv_dn"][i]
+        s = 1.0 / (1.0 - svd[4])
+        dec_gate = sv_d0[3] if i == 0 else None  # up_convs[0]'s input is dense_concats[0]'s output
+        d_res_pre, dx, d_cd = upconv_bwd(_pp(P, f"up_convs.{i}", UP), st["sv_up"][i], sink, dx,
+                                         res_gate=svd[3], res_gate_scale=s, dec_gate=dec_gate,
+                                         dec_gate_scale=1.0 / (1.0 - sv_d0[4]))
+        if i < 2:
+            d_conds[(i - 1) % 2] = d_cd
+        d_midi, d_audio = dense_bwd(_pp(P, f"dense_concats.{i + 1}", DN), svd, sink, d_res_pre,
+                                    gated=True)
+        d_before_m[depth - 2 - i] = d_midi
+        d_before_a[depth - 2 - i] = d_audio
+    d_xm, d_xa = dense_bwd(_pp(P, "dense_concats.0", DN), sv_d0, sink, dx, gated=True)
+    del dx
+    # onset/offset encoder: level 2 pooled = conds[1], level 1 pooled = conds[0] and level-2 input
+    sv_o = st["sv_o"]
+    d2 = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.2", DC), sv_o[2], sink,
+                      d_pool0=d_conds[1])
+    d1 = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.1", DC), sv_o[1], sink,
+                      d_pool0=d_conds[0], d_pool1=d2)
+    del d2
+    d_cond_in = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.0", DC), sv_o[0], sink,
+                             d_pool0=d1, need_dx=need_input_grads[2])
+    del d1
+    grads_in = []
+    for name, sv, d_before, d_top in (("down_convs", st["sv_m"], d_before_m, d_xm),
+                                      ("down_convs_audio", st["sv_a"], d_before_a, d_xa)):
+        d_pool = None
+        for i in reversed(range(depth)):
+            prm = _pp(P, f"{name}.{i}", DC)
+            if i == depth - 1:  # no pooling: before_pool is the output
+                d_pool = downconv_bwd(prm, sv[i], sink, d_before=d_top, need_dx=True)
+            else:
+                need = i > 0 or need_input_grads[0 if name == "down_convs" else 1]
+                d_pool = downconv_bwd(prm, sv[i], sink, d_before=d_before[i], d_pool0=d_pool,
+                                      need_dx=need)
+            d_before[i] = None
+        grads_in.append(d_pool)
+    return grads_in[0], grads_in[1], d_cond_in
+
+
+class PerformanceNetFunction(torch.autograd.Function):
+    """One autograd node for the whole network. Inputs: (module, x_midi, x_audio, cond, *params)."""
+
+    @staticmethod
+    def forward(ctx, module, x_midi, x_audio, cond, *params):
+        P = module._param_dict()
+        drop_p = module._dropout_p() if module.training else 0.0
+        seed = module._next_seed() if drop_p > 0 else 0
+        xm, xa, cd = (t if t.stride(2) == 1 and t.dtype == torch.float32 else t.float().contiguous()
+                      for t in (x_midi, x_audio, cond))
+        y, state = network_fwd(P, xm, xa, cd, drop_p, seed, module.depth)
+        ctx.module = module
+        ctx.state = state
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        module = ctx.module
+        P = module._param_dict()
+        need = (ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+        g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), module._grad_sink(), need)
+        ctx.state = None
+        n_params = len(module._flat_params_list())
+        return (None, g_m if need[0] else None, g_a if need[1] else None,
+                g_c if need[2] else None) + (None,) * n_params
+
+
+class L1LossFunction(torch.autograd.Function):
+    """nn.L1Loss() (train.py:132): mean |pred - target| on the device."""
+
+    @staticmethod
+    def forward(ctx, pred, target):
+        pred = pred.contiguous()
+        target = target.contiguous()
+        ctx.save_for_backward(pred, target)
+        return K.l1_fwd(pred, target)
+
+    @staticmethod
+    def backward(ctx, g):
+        pred, target = ctx.saved_tensors
+        return K.l1_bwd(pred, target, g.contiguous()), None
+
+
+def l1_loss(pred, target):
+    return L1LossFunction.apply(pred, target)
+
+
+def mse_loss(pred, target):
+    """nn.MSELoss() forward (test(), train.py:158); evaluation only."""
+    return K.mse_fwd(pred.contiguous(), target.contiguous())

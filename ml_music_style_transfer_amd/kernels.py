@@ -1,0 +1,322 @@
+"""Thin tensor-level wrappers over libmst_hip's C ABI (include/mst.h).
+
+Every function enqueues HIP kernels on torch's current stream and returns
+without synchronising. Tensors must be contiguous float32 CUDA tensors; there
+is deliberately no CPU fallback (see _lib.ptr).
+
+Layer geometry (all implicit GEMMs of gemm.hip; reference model/model.py):
+  conv3   nn.Conv1d(k=3, p=1)                       model.py:14-22
+  convT2  nn.ConvTranspose1d(k, s=2, p=1)           model.py:24-31   (two sub-pixel phases)
+  convT1  nn.ConvTranspose1d(k=3, s=1, p=1)         model.py:242     (lastconv)
+  linear  nn.Linear over channels of an NCL tensor  model.py:98-99,104-107
+Sources are (tensor, time_offset) pairs forming a virtual channel concat; the
+offset implements crop_and_concat (model.py:71-78).
+"""
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+SLOPE = 0.01
+IN_EPS = 1e-5
+
+
+def _lib():
+    return L.load()
+
+
+def empty(*shape, like=None, device=None):
+    dev = like.device if like is not None else device
+    return torch.empty(shape, device=dev, dtype=torch.float32)
+
+
+def _src(spec):
+    s = L.MstSrc()
+    if spec is None:
+        return s
+    t, off = spec
+    # any NCL view with unit time stride works (e.g. the channel halves of torch.split, train.py:130)
+    assert t.dim() == 3 and t.stride(2) == 1 and t.dtype == torch.float32 and t.is_cuda
+    s.p = t.data_ptr()
+    s.sb = t.stride(0)
+    s.sc = t.stride(1)
+    s.C = t.shape[1]
+    s.T = t.shape[2]
+    s.off = off
+    return s
+
+
+def _dst(spec):
+    d = L.MstDst()
+    if spec is None:
+        return d
+    t, off, gate, gscale = spec
+    assert t.is_contiguous() and t.dim() == 3
+    d.p = t.data_ptr()
+    d.sb = t.shape[1] * t.shape[2]
+    d.sc = t.shape[2]
+    d.C = t.shape[1]
+    d.T = t.shape[2]
+    d.off = off
+    if gate is not None:
+        assert gate.shape == t.shape
+        d.gate = gate.data_ptr()
+        d.gate_scale = gscale
+    return d
+
+
+def _workspace(nbytes, device):
+    if nbytes == 0:
+        return None, 0
+    return torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32), nbytes
+
+
+# Optional per-launch GEMM timing (bench.py's roofline leg): when a list is installed, every
+# GEMM launch is bracketed by HIP events on torch's current stream (the launch stream).
+_GEMM_LOG = None
+
+
+def gemm_timing(log):
+    """Install (list) or remove (None) the GEMM timing log; entries are (start, end, flops, tag)."""
+    global _GEMM_LOG
+    _GEMM_LOG = log
+
+
+def _timed(launch, flops, tag):
+    if _GEMM_LOG is None:
+        launch()
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
+    launch()
+    e.record()
+    _GEMM_LOG.append((s, e, flops, tag))
+
+
+def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt, dsts, ostride=1,
+              ophase=0, alpha=1.0, bias=None, act=L.ACT_NONE, drop_p=0.0, seed=0, splitk=0):
+    lib = _lib()
+    d = L.MstConvDesc()
+    d.B, d.M, d.Tn, d.taps = B, M, Tn, taps
+    d.Ctot = sum(s[0].shape[1] for s in srcs)
+    d.a, d.beta, d.g, d.Tv = a, beta, g, Tv
+    d.A = A.data_ptr() + 4 * A_off
+    d.sAm, d.sAc, d.sAt = sAm, sAc, sAt
+    d.src[0] = _src(srcs[0])
+    d.src[1] = _src(srcs[1] if len(srcs) > 1 else None)
+    d.ostride, d.ophase = ostride, ophase
+    d.dst[0] = _dst(dsts[0])
+    d.dst[1] = _dst(dsts[1] if len(dsts) > 1 else None)
+    d.alpha = alpha
+    d.bias = bias.data_ptr() if bias is not None else None
+    d.act = act
+    d.drop_p = drop_p
+    d.seed = seed
+    d.splitk = splitk
+    ref = ctypes.byref(d)
+    ws, nb = _workspace(lib.mst_conv_fwd_workspace_size(ref), A.device)
+    _timed(lambda: L.check(lib.mst_conv_fwd_f32(ref, L.ptr(ws), nb, L.stream()), "mst_conv_fwd_f32"),
+           2.0 * M * B * Tn * d.Ctot * taps, "conv")
+
+
+def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate=False, splitk=0):
+    lib = _lib()
+    d = L.MstWgradDesc()
+    B, M, Tk = P.shape
+    d.B, d.M, d.Tk, d.taps = B, M, Tk, taps
+    d.Ctot = sum(s[0].shape[1] for s in srcs)
+    d.a, d.beta, d.g, d.Tv = a, beta, g, Tv
+    d.P = P.data_ptr()
+    d.sPb = M * Tk
+    d.sPc = Tk
+    d.src[0] = _src(srcs[0])
+    d.src[1] = _src(srcs[1] if len(srcs) > 1 else None)
+    d.out = out.data_ptr()
+    d.ldo = ldo
+    d.scale = scale
+    d.accumulate = 1 if accumulate else 0
+    d.splitk = splitk
+    ref = ctypes.byref(d)
+    ws, nb = _workspace(lib.mst_wgrad_workspace_size(ref), P.device)
+    _timed(lambda: L.check(lib.mst_conv_wgrad_f32(ref, L.ptr(ws), nb, L.stream()),
+                           "mst_conv_wgrad_f32"), 2.0 * M * B * Tk * d.Ctot * taps, "wgrad")
+
+
+# ---------------------------------------------------------------- Conv1d k3 p1
+def conv3_fwd(srcs, W, bias, out, act=L.ACT_NONE):
+    B, Cout, T = out.shape
+    Cin = W.shape[1]
+    conv_like(B=B, M=Cout, Tn=T, srcs=srcs, Tv=T, taps=3, a=1, beta=-1, g=1, A=W, sAm=Cin * 3,
+              sAc=3, sAt=1, dsts=[(out, 0, None, 1.0)], bias=bias, act=act)
+
+
+def conv3_dgrad(dY, W, dsts):
+    B, Cout, T = dY.shape
+    Cin = W.shape[1]
+    conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=3, a=1, beta=1, g=-1, A=W, sAm=3,
+              sAc=Cin * 3, sAt=1, dsts=dsts)
+
+
+def conv3_wgrad(dY, srcs, dW, accumulate):
+    Cin = dW.shape[1]
+    wgrad_like(P=dY, srcs=srcs, Tv=dY.shape[2], taps=3, a=1, beta=-1, g=1, out=dW, ldo=Cin * 3,
+               accumulate=accumulate)
+
+
+# ------------------------------------------------- ConvTranspose1d(k, s=2, p=1)
+def convT2_out_len(Tin, k):
+    return (Tin - 1) * 2 - 2 + k
+
+
+def convT2_fwd(x, W, bias, out):
+    Cin, Cout, k = W.shape
+    B, _, Tin = x.shape
+    Tout = out.shape[2]
+    for p in (0, 1):
+        nq = k // 2 if p == 0 else (k + 1) // 2
+        Tn = (Tout - p + 1) // 2
+        if nq == 0 or Tn <= 0:
+            continue
+        conv_like(B=B, M=Cout, Tn=Tn, srcs=[(x, 0)], Tv=Tin, taps=nq, a=1, beta=p, g=-1, A=W,
+                  A_off=1 - p, sAm=k, sAc=Cout * k, sAt=2, dsts=[(out, 0, None, 1.0)], ostride=2,
+                  ophase=p, bias=bias)
+
+
+def convT2_dgrad(dY, W, dsts):
+    Cin, Cout, k = W.shape
+    B, _, Tout = dY.shape
+    Tin = dsts[0][0].shape[2]
+    conv_like(B=B, M=Cin, Tn=Tin, srcs=[(dY, 0)], Tv=Tout, taps=k, a=2, beta=-1, g=1, A=W,
+              sAm=Cout * k, sAc=k, sAt=1, dsts=dsts)
+
+
+def convT2_wgrad(x, dY, dW, accumulate):
+    Cin, Cout, k = dW.shape
+    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=k, a=2, beta=-1, g=1, out=dW,
+               ldo=Cout * k, accumulate=accumulate)
+
+
+# ------------------------------------------- ConvTranspose1d(k=3, s=1, p=1) (lastconv)
+def convT1_fwd(x, W, bias, out, alpha=1.0, act=L.ACT_NONE):
+    Cin, Cout, k = W.shape
+    B, _, T = x.shape
+    conv_like(B=B, M=Cout, Tn=T, srcs=[(x, 0)], Tv=T, taps=k, a=1, beta=1, g=-1, A=W, sAm=k,
+              sAc=Cout * k, sAt=1, dsts=[(out, 0, None, 1.0)], alpha=alpha, bias=bias, act=act)
+
+
+def convT1_dgrad(dY, W, dx, alpha=1.0):
+    Cin, Cout, k = W.shape
+    B, _, T = dY.shape
+    conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=k, a=1, beta=-1, g=1, A=W,
+              sAm=Cout * k, sAc=k, sAt=1, dsts=[(dx, 0, None, 1.0)], alpha=alpha)
+
+
+def convT1_wgrad(x, dY, dW, accumulate, scale=1.0):
+    Cin, Cout, k = dW.shape
+    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=k, a=1, beta=-1, g=1, out=dW,
+               ldo=Cout * k, scale=scale, accumulate=accumulate)
+
+
+# ------------------------------------------------------- Linear over NCL channels
+def linear_fwd(srcs, W, bias, out, act=L.ACT_NONE, drop_p=0.0, seed=0):
+    B, Cout, T = out.shape
+    Cin = W.shape[1]
+    conv_like(B=B, M=Cout, Tn=T, srcs=srcs, Tv=T, taps=1, a=1, beta=0, g=0, A=W, sAm=Cin, sAc=1,
+              sAt=1, dsts=[(out, 0, None, 1.0)], bias=bias, act=act, drop_p=drop_p, seed=seed)
+
+
+def linear_dgrad(dY, W, dsts):
+    B, Cout, T = dY.shape
+    Cin = W.shape[1]
+    conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=1, a=1, beta=0, g=0, A=W, sAm=1,
+              sAc=Cin, sAt=1, dsts=dsts)
+
+
+def linear_wgrad(dY, srcs, dW, accumulate):
+    wgrad_like(P=dY, srcs=srcs, Tv=dY.shape[2], taps=1, a=1, beta=0, g=0, out=dW,
+               ldo=dW.shape[1], accumulate=accumulate)
+
+
+# ---------------------------------------------------------- norm / elementwise
+def in_lrelu_fwd(y, pool):
+    B, C, T = y.shape
+    a = torch.empty_like(y)
+    pooled = empty(B, C, T // 2, like=y) if pool else None
+    mean = empty(B * C, like=y)
+    rstd = empty(B * C, like=y)
+    L.check(_lib().mst_instnorm_lrelu_fwd_f32(L.ptr(y), B * C, T, IN_EPS, SLOPE, L.ptr(a),
+                                              L.ptr(pooled), L.ptr(mean), L.ptr(rstd), L.stream()),
+            "instnorm_fwd")
+    return a, pooled, mean, rstd
+
+
+def in_lrelu_bwd(y, mean, rstd, d_a=None, d_pool0=None, d_pool1=None):
+    B, C, T = y.shape
+    dy = torch.empty_like(y)
+    L.check(_lib().mst_instnorm_lrelu_bwd_f32(L.ptr(y), L.ptr(mean), L.ptr(rstd), B * C, T, SLOPE,
+                                              L.ptr(d_a), L.ptr(d_pool0), L.ptr(d_pool1), L.ptr(dy),
+                                              L.stream()), "instnorm_bwd")
+    return dy
+
+
+def bias_grad(dy, db, accumulate):
+    B, C, T = dy.shape
+    L.check(_lib().mst_bias_grad_f32(L.ptr(dy), B, C, T, 1.0, L.ptr(db), 1 if accumulate else 0,
+                                     L.stream()), "bias_grad")
+
+
+def lrelu_bwd(dy, y):
+    dx = torch.empty_like(y)
+    L.check(_lib().mst_lrelu_bwd_f32(L.ptr(dy), L.ptr(y), y.numel(), SLOPE, L.ptr(dx), L.stream()),
+            "lrelu_bwd")
+    return dx
+
+
+def relu_gate_bwd(d, h, scale):
+    out = torch.empty_like(h)
+    L.check(_lib().mst_relu_gate_bwd_f32(L.ptr(d), L.ptr(h), h.numel(), scale, L.ptr(out),
+                                         L.stream()), "relu_gate_bwd")
+    return out
+
+
+def _loss(fn, pred, target):
+    lib = _lib()
+    n = pred.numel()
+    ws = torch.empty(lib.mst_l1_workspace_size(n) // 4 + 2, device=pred.device, dtype=torch.float32)
+    loss = torch.empty((), device=pred.device, dtype=torch.float32)
+    L.check(getattr(lib, fn)(L.ptr(pred), L.ptr(target), n, L.ptr(loss), L.ptr(ws), L.stream()), fn)
+    return loss
+
+
+def l1_fwd(pred, target):
+    return _loss("mst_l1_fwd_f32", pred, target)
+
+
+def mse_fwd(pred, target):
+    return _loss("mst_mse_fwd_f32", pred, target)
+
+
+def l1_bwd(pred, target, gscale):
+    dx = torch.empty_like(pred)
+    L.check(_lib().mst_l1_bwd_f32(L.ptr(pred), L.ptr(target), pred.numel(), L.ptr(gscale), L.ptr(dx),
+                                  L.stream()), "l1_bwd")
+    return dx
+
+
+def adam(p, g, m, v, lr_step, b1, b2, eps, bc2_sqrt):
+    L.check(_lib().mst_adam_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step, b1, b2,
+                                eps, bc2_sqrt, L.stream()), "adam")
+
+
+def scale_(x, s):
+    L.check(_lib().mst_scale_f32(L.ptr(x), x.numel(), s, L.stream()), "scale")
+
+
+def fill_(x, v):
+    L.check(_lib().mst_fill_f32(L.ptr(x), x.numel(), v, L.stream()), "fill")
+
+
+def axpby_(x, y, a, b):
+    L.check(_lib().mst_axpby_f32(L.ptr(x), L.ptr(y), x.numel(), a, b, L.stream()), "axpby")

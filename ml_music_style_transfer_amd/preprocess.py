@@ -1,0 +1,144 @@
+"""Drop-in for the reference front end (preprocessing/preprocess.py), on the device.
+
+`process_spectrum_from_chunk` keeps the reference signature and returns the
+same (1025, 1 + L//256) float32 array type it was given (NumPy in -> NumPy out,
+CUDA tensor in -> CUDA tensor out); the STFT itself always runs in libmst_hip.
+The integer chunk/frame arithmetic is the reference's, bit for bit.
+File globbing, zip extraction, librosa.load/pretty_midi file parsing and HDF5
+writing (preprocess.py:99-116,139-147,163-214) are offline I/O outside this path.
+"""
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import spectral
+
+
+class hyperparams(object):
+    """preprocess.py:17-42 (framing constants)."""
+
+    def __init__(self, sr=44100, n_fft=2048, stride=512, ws=256, spc=5):
+        self.sr = sr
+        self.n_fft = n_fft
+        self.stride = stride
+        self.piano_scores = {
+            'train': [2240, 2530, 1763, 2308, 2533, 1772, 2444, 2478,
+                      2509, 1776, 1749, 2486, 2487, 2678, 2490, 2492, 2527],
+            'test': [2533, 1760],
+        }
+        self.styles = ['cuba', 'aliciakeys', 'gentleman', 'harpsichord', 'upright']
+        self.ws = ws
+        self.wps = self.sr // self.ws
+        self.spc = spc
+
+
+hp = hyperparams()
+
+
+def _to_device(x):
+    if isinstance(x, torch.Tensor):
+        return (x if x.is_cuda else x.cuda()).float(), "torch_cuda" if x.is_cuda else "torch_cpu"
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).cuda(), "numpy"
+
+
+def _back(t, kind):
+    if kind == "numpy":
+        return t.cpu().numpy()
+    if kind == "torch_cpu":
+        return t.cpu()
+    return t
+
+
+def process_spectrum_from_chunk(audio_chunk, hop=None, pad_mode="reflect"):
+    """preprocess.py:47-49: log1p(|stft(audio_chunk, n_fft=2048, hop_length=256)|^2).
+    Accepts (L,) or a batch (B, L)."""
+    x, kind = _to_device(audio_chunk)
+    out = spectral.stft_logpow(x, hop=hop or hp.ws, n_fft=hp.n_fft, pad_mode=pad_mode)
+    return _back(out, kind)
+
+
+def chunk_bounds_audio(step, h=hp):
+    """preprocess.py:66-67."""
+    n = (h.spc * h.wps - 1) * h.ws
+    s = step * h.ws * h.stride
+    return s, s + n
+
+
+def chunk_bounds_roll(step, h=hp):
+    """preprocess.py:86-87."""
+    n = h.spc * h.wps
+    s = step * h.stride
+    return s, s + n
+
+
+def process_audio_into_chunks(audio, style, song_id, num_chunks, debug=False, h=hp):
+    """preprocess.py:60-77, with every chunk's STFT batched into one kernel launch."""
+    print(f"processing {style} style for song_id {song_id}")
+    x, kind = _to_device(audio)
+    chunks = []
+    for step in range(num_chunks):
+        s, e = chunk_bounds_audio(step, h)
+        chunks.append(x[s:e])
+    if not chunks:
+        return np.zeros((0,)) if kind == "numpy" else torch.zeros(0)
+    n = (h.spc * h.wps - 1) * h.ws
+    if all(c.shape[0] == n for c in chunks):
+        out = spectral.stft_logpow(torch.stack(chunks), hop=h.ws, n_fft=h.n_fft)
+        return _back(out, kind)
+    outs = [spectral.stft_logpow(c, hop=h.ws, n_fft=h.n_fft) for c in chunks]  # ragged tail
+    return np.array([_back(o, kind) for o in outs], dtype=object) if kind == "numpy" else outs
+
+
+def process_pianoroll_into_chunks(pianoroll, onoff, song_id, num_chunks, debug=False, h=hp):
+    """preprocess.py:80-96 (pure slicing)."""
+    print(f"processing pianoroll for song_id {song_id}")
+    score_list, onoff_list = [], []
+    for step in range(num_chunks):
+        s, e = chunk_bounds_roll(step, h)
+        score_list.append(pianoroll[s:e])
+        onoff_list.append(onoff[s:e])
+    return np.array(score_list), np.array(onoff_list)
+
+
+def get_num_song_chunks(pianoroll, offset_percentage=0.1, max_chunks=100, h=hp):
+    """preprocess.py:118-136."""
+    n_windows_per_chunk = h.spc * h.wps
+    num_chunks = (pianoroll.shape[0] - n_windows_per_chunk) // h.stride
+    offset = int(offset_percentage * num_chunks)
+    num_chunks -= offset
+    if num_chunks > max_chunks:
+        print(f"song has more than max_chunks={max_chunks}, reducing")
+        num_chunks = max_chunks
+    print('song has {} chunks'.format(num_chunks))
+    return num_chunks
+
+
+def pianoroll_onoff(roll):
+    """preprocess.py:147-155 on the device: roll (T, 128) or (B, T, 128) velocities ->
+    (binarised roll, onoff) with onoff[t] = roll[t] - roll[t-1] in {-1, 0, 1}."""
+    x, kind = _to_device(roll)
+    single = x.dim() == 2
+    if single:
+        x = x.unsqueeze(0)
+    x = x.contiguous()
+    B, T, P = x.shape
+    if P != 128:
+        raise ValueError("piano roll must have 128 pitches on the last axis")
+    b = torch.empty_like(x)
+    o = torch.empty_like(x)
+    L.check(L.load().mst_onoff_f32(L.ptr(x), B, T, L.ptr(b), L.ptr(o), L.stream()), "onoff")
+    if single:
+        b, o = b[0], o[0]
+    return _back(b, kind), _back(o, kind)
+
+
+def piano_roll_from_notes(notes, fs, n_frames=None):
+    """pretty_midi.PrettyMIDI.get_piano_roll(fs) for a note list (pitch, start_s, end_s, velocity)
+    without sustain-pedal events (preprocess.py:147): (128, n) float64."""
+    notes = list(notes)
+    end = max((n[2] for n in notes), default=0.0)
+    n = int(fs * end) if n_frames is None else n_frames
+    roll = np.zeros((128, n), dtype=np.float64)
+    for p, s, e, v in notes:
+        roll[int(p), int(s * fs):int(e * fs)] += v
+    return roll

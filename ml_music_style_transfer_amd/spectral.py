@@ -1,0 +1,197 @@
+"""Device front end: STFT log-power / power / complex, mel spectrogram, iSTFT, Griffin-Lim.
+
+Semantics follow the reference's librosa calls (librosa 0.7-0.9: Hann periodic
+window, center=True, reflect padding, n_fft=2048):
+  logpow       preprocessing/preprocess.py:47-49   np.log1p(np.abs(librosa.stft(y, 2048, 256))**2)
+  melspec      tests/plot_spec.py:20                librosa.feature.melspectrogram (slaney, 128 mels)
+  griffinlim   model/inference.py:105-110          librosa.griffinlim(n_iter, momentum=0.99)
+All compute runs in libmst_hip's FFT kernels (fft.hip); inputs/outputs are CUDA tensors.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+N_FFT = 2048
+
+
+def _as_batch(x):
+    if x.dim() == 1:
+        return x.unsqueeze(0), True
+    return x, False
+
+
+def _check_signal(x):
+    if not x.is_cuda:
+        raise RuntimeError("spectral kernels need a CUDA tensor")
+    return x.contiguous().float()
+
+
+def n_frames(L_samples, hop):
+    return 1 + L_samples // hop
+
+
+def stft_logpow(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
+    """(L,) or (B, L) signal -> (F, T) / (B, F, T) log1p(|STFT|^2)."""
+    return _stft_real("mst_stft_logpow_f32", x, hop, n_fft, pad_mode)
+
+
+def stft_power(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
+    """|STFT|^2, same layout as stft_logpow."""
+    return _stft_real("mst_stft_power_f32", x, hop, n_fft, pad_mode)
+
+
+def _pad_code(pad_mode):
+    return {"reflect": L.PAD_REFLECT, "constant": L.PAD_CONSTANT}[pad_mode]
+
+
+def _stft_real(fn, x, hop, n_fft, pad_mode):
+    x, single = _as_batch(_check_signal(x))
+    B, Ls = x.shape
+    T = n_frames(Ls, hop)
+    out = torch.empty(B, n_fft // 2 + 1, T, device=x.device, dtype=torch.float32)
+    L.check(getattr(L.load(), fn)(L.ptr(x), B, Ls, n_fft, hop, _pad_code(pad_mode), L.ptr(out),
+                                  L.stream()), fn)
+    return out[0] if single else out
+
+
+def stft_complex(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
+    """Complex STFT, frame-major: (B, T, F) complex64 view of a (B, T, F, 2) buffer."""
+    x, single = _as_batch(_check_signal(x))
+    B, Ls = x.shape
+    T = n_frames(Ls, hop)
+    out = torch.empty(B, T, n_fft // 2 + 1, 2, device=x.device, dtype=torch.float32)
+    L.check(L.load().mst_stft_complex_f32(L.ptr(x), B, Ls, n_fft, hop, _pad_code(pad_mode),
+                                          L.ptr(out), L.stream()), "stft_complex")
+    out = torch.view_as_complex(out)
+    return out[0] if single else out
+
+
+def istft(X, hop=256):
+    """Inverse of stft_complex: (B, T, F) complex (frame-major) -> (B, hop*(T-1))."""
+    single = X.dim() == 2
+    if single:
+        X = X.unsqueeze(0)
+    Xr = torch.view_as_real(X.contiguous()).contiguous()
+    B, T, F, _ = Xr.shape
+    y = torch.empty(B, hop * (T - 1), device=X.device, dtype=torch.float32)
+    L.check(L.load().mst_istft_f32(L.ptr(Xr), B, F, T, hop, L.ptr(y), L.stream()), "istft")
+    return y[0] if single else y
+
+
+# ------------------------------------------------------------------- mel
+def _hz_to_mel(f):
+    f = np.asarray(f, dtype=np.float64)
+    f_sp = 200.0 / 3
+    lin = f / f_sp
+    log_t = 1000.0 / f_sp + np.log(np.maximum(f, 1e-300) / 1000.0) / (np.log(6.4) / 27.0)
+    return np.where(f >= 1000.0, log_t, lin)
+
+
+def _mel_to_hz(m):
+    m = np.asarray(m, dtype=np.float64)
+    f_sp = 200.0 / 3
+    min_log_mel = 1000.0 / f_sp
+    return np.where(m >= min_log_mel, 1000.0 * np.exp(np.log(6.4) / 27.0 * (m - min_log_mel)), f_sp * m)
+
+
+def mel_basis(sr, n_fft=N_FFT, n_mels=128, fmin=0.0, fmax=None):
+    """Slaney-normalised mel filterbank (librosa.filters.mel defaults) as float32 (n_mels, F)."""
+    fmax = sr / 2.0 if fmax is None else fmax
+    nb = 1 + n_fft // 2
+    fftfreqs = np.linspace(0, sr / 2.0, nb)
+    mel_f = _mel_to_hz(np.linspace(_hz_to_mel(fmin), _hz_to_mel(fmax), n_mels + 2))
+    fdiff = np.diff(mel_f)
+    ramps = mel_f[:, None] - fftfreqs[None, :]
+    lower = -ramps[:-2] / fdiff[:-1, None]
+    upper = ramps[2:] / fdiff[1:, None]
+    w = np.maximum(0, np.minimum(lower, upper))
+    w *= (2.0 / (mel_f[2:n_mels + 2] - mel_f[:n_mels]))[:, None]
+    return w.astype(np.float32)
+
+
+_MEL_CACHE = {}
+
+
+def _mel_tables(sr, n_fft, n_mels, device):
+    key = (sr, n_fft, n_mels, str(device))
+    if key not in _MEL_CACHE:
+        w = mel_basis(sr, n_fft, n_mels)
+        start, length, woff, vals = [], [], [], []
+        off = 0
+        for m in range(n_mels):
+            nz = np.nonzero(w[m])[0]
+            s, e = (int(nz[0]), int(nz[-1]) + 1) if nz.size else (0, 0)
+            start.append(s)
+            length.append(e - s)
+            woff.append(off)
+            vals.append(w[m, s:e])
+            off += e - s
+        vals = np.concatenate(vals) if off else np.zeros(1, np.float32)
+        mk = lambda a, dt: torch.tensor(np.asarray(a), dtype=dt, device=device)  # noqa: E731
+        _MEL_CACHE[key] = (mk(start, torch.int32), mk(length, torch.int32), mk(woff, torch.int32),
+                           mk(vals, torch.float32))
+    return _MEL_CACHE[key]
+
+
+def melspectrogram(x, sr, n_fft=N_FFT, hop_length=256, n_mels=128, pad_mode="reflect"):
+    """librosa.feature.melspectrogram(y, sr, n_fft, hop_length) (power 2, slaney, 128 mels)."""
+    x, single = _as_batch(_check_signal(x))
+    B, Ls = x.shape
+    T = n_frames(Ls, hop_length)
+    st, ln, wo, w = _mel_tables(sr, n_fft, n_mels, x.device)
+    out = torch.empty(B, n_mels, T, device=x.device, dtype=torch.float32)
+    L.check(L.load().mst_stft_mel_f32(L.ptr(x), B, Ls, n_fft, hop_length, _pad_code(pad_mode),
+                                      L.ptr(st), L.ptr(ln), L.ptr(wo), L.ptr(w), n_mels, L.ptr(out),
+                                      L.stream()), "stft_mel")
+    return out[0] if single else out
+
+
+# ------------------------------------------------------------ Griffin-Lim
+def random_angles(shape_btf, seed, device):
+    """Unit phases exp(2 pi i U[0,1)) like librosa's init='random' (seeded), frame-major."""
+    rng = np.random.RandomState(seed)
+    ang = np.exp(2j * np.pi * rng.rand(*shape_btf)).astype(np.complex64)
+    return torch.view_as_real(torch.from_numpy(ang)).contiguous().to(device)
+
+
+def griffinlim(S, n_iter=60, hop_length=256, momentum=0.99, init="random", seed=0,
+               from_logpow=False):
+    """librosa.griffinlim on the device. S: (F, T) or (B, F, T) magnitudes (or log-power when
+    from_logpow, inverted as sqrt(expm1(clip(S, 0, 20))) like inference.py:109).
+    init: 'random' (seeded), None/'ones', or a (B, T, F, 2) float tensor of unit phases."""
+    S, single = (S.unsqueeze(0), True) if S.dim() == 2 else (S, False)
+    S = S.contiguous().float()
+    if not S.is_cuda:
+        raise RuntimeError("griffinlim needs a CUDA tensor")
+    B, F, T = S.shape
+    if momentum < 0:
+        raise ValueError("griffinlim() called with momentum < 0")
+    if isinstance(init, torch.Tensor):
+        ang = init.contiguous().float()
+    elif init == "random":
+        ang = random_angles((B, T, F), seed, S.device)
+    elif init is None or init == "ones":
+        ang = None
+    else:
+        raise ValueError(f"init={init!r} must be 'random', None or a tensor")
+    lib = L.load()
+    nbytes = lib.mst_griffinlim_workspace_size(B, F, T, hop_length)
+    ws = torch.empty(nbytes // 4 + 64, device=S.device, dtype=torch.float32)
+    y = torch.empty(B, hop_length * (T - 1), device=S.device, dtype=torch.float32)
+    L.check(lib.mst_griffinlim_f32(L.ptr(S), B, F, T, hop_length, n_iter, float(momentum),
+                                   L.ptr(ang), 1 if from_logpow else 0, L.ptr(y), L.ptr(ws),
+                                   ws.numel() * 4, L.stream()), "griffinlim")
+    return y[0] if single else y
+
+
+def spectral_convergence(S, y, hop=256):
+    """|| |STFT(y)| - S ||_F / ||S||_F for (B, F, T) magnitudes (diagnostic)."""
+    P = stft_power(y, hop).clamp_min(0).sqrt()
+    return (torch.linalg.vector_norm(P - S) / torch.linalg.vector_norm(S)).item()
+
+
+__all__ = ["stft_logpow", "stft_power", "stft_complex", "istft", "melspectrogram", "mel_basis",
+           "griffinlim", "random_angles", "spectral_convergence", "n_frames", "math"]

@@ -1,0 +1,256 @@
+"""Drop-in for the reference training step API (model/train.py).
+
+`train(model, epoch, train_loader, optimizer, iter_train_loss)` and
+`test(model, epoch, test_loader, scheduler, iter_test_loss)` keep the
+reference's signatures, loop structure, prints and return values
+(train.py:125-170); the loss is the device L1 (engine.l1_loss) and `Adam`
+is a torch.optim.Optimizer whose step runs one fused kernel over the model's
+flat parameter buffer (torch.optim.Adam semantics, state_dict format included,
+so ReduceLROnPlateau and checkpointing work unchanged).
+
+The HDF5 data path (Dataseth5py / Process_Data, train.py:45-116) needs h5py,
+which this image lacks: `SyntheticSpectrogramDataset` produces batches of the
+same (data (B,256,T), data_cond (B,1025,T), target (B,1025,T)) shape instead.
+"""
+import argparse
+import json
+import math
+import os
+
+import numpy as np
+import torch
+
+from . import engine as E
+from . import kernels as K
+from .model import PerformanceNet
+
+
+class hyperparams(object):
+    """train.py:32-42."""
+
+    def __init__(self, args):
+        self.train_epoch = args.epochs
+        self.test_freq = args.test_freq
+        self.exp_name = args.exp_name
+        self.iter_train_loss = []
+        self.iter_test_loss = []
+        self.loss_history = []
+        self.test_loss_history = []
+        self.best_loss = 1e10
+        self.best_epoch = 0
+
+
+class Adam(torch.optim.Optimizer):
+    """torch.optim.Adam (no weight decay / amsgrad) with a fused device update.
+
+    When every parameter of a group with a gradient lives in one PerformanceNet flat
+    buffer (and its gradient in the matching flat gradient buffer) the update is one
+    kernel launch over the whole buffer; otherwise one launch per parameter.
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                 amsgrad=False):
+        if weight_decay != 0 or amsgrad:
+            raise NotImplementedError("the reference uses Adam(lr=1e-3) only (train.py:188)")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False))
+        self._flat_groups = {}
+
+    def _flat_of(self, group, params):
+        """Return (flat_param, flat_grad, numel, offsets) if params tile one model's flat buffers."""
+        ref = getattr(params[0], "_mst_flat_owner", None)
+        owner = ref() if ref is not None else getattr(self, "_owner", None)
+        if owner is None or not owner._flat_ok():
+            return None
+        self._owner = owner
+        pf, gf, n = owner.flat_buffers()
+        index = owner._flat["index"]
+        if len(params) != len(index):
+            return None
+        base_p, base_g = pf.data_ptr(), gf.data_ptr()
+        for p in params:
+            ent = index.get(id(p))
+            if ent is None or p.grad is None:
+                return None
+            o = ent[0]
+            if p.data_ptr() != base_p + 4 * o or p.grad.data_ptr() != base_g + 4 * o:
+                return None
+        return pf, gf, n
+
+    def attach(self, model):
+        """Declare the PerformanceNet whose flat buffers the parameters live in."""
+        self._owner = model
+        return self
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            b1, b2 = group["betas"]
+            lr, eps = group["lr"], group["eps"]
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
+                continue
+            flat = self._flat_of(group, params)
+            if flat is not None:
+                pf, gf, n = flat
+                key = (gi, pf.data_ptr())
+                st = self._flat_groups.get(key)
+                if st is None:
+                    m = torch.zeros_like(pf)
+                    v = torch.zeros_like(pf)
+                    st = {"m": m, "v": v, "step": 0}
+                    self._flat_groups[key] = st
+                    index = self._owner._flat["index"]
+                    for p in params:
+                        o, k = index[id(p)]
+                        self.state[p] = {"step": None, "exp_avg": m[o:o + k].view_as(p),
+                                         "exp_avg_sq": v[o:o + k].view_as(p)}
+                st["step"] += 1
+                t = st["step"]
+                bc1 = 1 - b1 ** t
+                bc2 = 1 - b2 ** t
+                K.adam(pf, gf, st["m"], st["v"], lr / bc1, b1, b2, eps, math.sqrt(bc2))
+                step_t = torch.tensor(float(t))
+                for p in params:
+                    self.state[p]["step"] = step_t
+                continue
+            for p in params:
+                state = self.state[p]
+                if len(state) == 0 or state.get("exp_avg") is None:
+                    state["step"] = torch.tensor(0.0)
+                    state["exp_avg"] = torch.zeros_like(p)
+                    state["exp_avg_sq"] = torch.zeros_like(p)
+                state["step"] += 1
+                t = float(state["step"])
+                bc1 = 1 - b1 ** t
+                bc2 = 1 - b2 ** t
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                K.adam(p.data, g, state["exp_avg"], state["exp_avg_sq"], lr / bc1, b1, b2, eps,
+                       math.sqrt(bc2))
+        return loss
+
+
+def make_optimizer(model, lr=1e-3):
+    """optim.Adam(model.parameters(), lr=1e-3) (train.py:188) bound to the model's flat buffers."""
+    return Adam(model.parameters(), lr=lr).attach(model)
+
+
+def _cuda(t):
+    return t if t.is_cuda else t.cuda(non_blocking=True)
+
+
+def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2):
+    """train.py:125-149 (same loop, loss and prints)."""
+    model.train()
+    train_loss = 0
+    for batch_idx, (data, data_cond, target) in enumerate(train_loader):
+        optimizer.zero_grad()
+        split = torch.split(data, 128, dim=1)
+        y_pred = model(_cuda(split[0]), _cuda(data_cond), _cuda(split[1]))
+        loss = E.l1_loss(y_pred, _cuda(target))
+        loss.backward()
+        iter_train_loss.append(loss.item())
+        train_loss += loss
+        optimizer.step()
+        if log_every and batch_idx % log_every == 0:
+            print('Train Epoch: {} [{}/{} ({:.0f}%)]\t Loss: {:.6f}'.format(
+                epoch, batch_idx * len(data), len(train_loader.dataset),
+                100. * batch_idx / len(train_loader), loss.item() / len(data)))
+    print('====> Epoch: {} Average loss: {:.4f}'.format(epoch, train_loss / len(train_loader.dataset)))
+    return train_loss / len(train_loader.dataset)
+
+
+def test(model, epoch, test_loader, scheduler, iter_test_loss):
+    """train.py:152-170 (MSE on the device, ReduceLROnPlateau step)."""
+    with torch.no_grad():
+        model.eval()
+        test_loss = 0
+        for idx, (data, data_cond, target) in enumerate(test_loader):
+            split = torch.split(data, 128, dim=1)
+            y_pred = model(_cuda(split[0]), _cuda(data_cond), _cuda(split[1]))
+            loss = E.mse_loss(y_pred, _cuda(target))
+            iter_test_loss.append(loss.item())
+            test_loss += loss
+        test_loss /= len(test_loader.dataset)
+        scheduler.step(test_loss)
+        print('====> Test set loss: {:.4f}'.format(test_loss))
+        return test_loss
+
+
+class SyntheticSpectrogramDataset(torch.utils.data.Dataset):
+    """Stand-in for Dataseth5py (train.py:45-104) with the same item layout:
+    X = concat(pianoroll, onoff).T (256, T), X_cond = random same-style spec, y = spec."""
+
+    def __init__(self, n, T=252, seed=0, device="cuda"):
+        g = torch.Generator().manual_seed(seed)
+        roll = (torch.rand(n, 128, T, generator=g) < 0.08).float()
+        prev = torch.cat([torch.zeros(n, 128, 1), roll[:, :, :-1]], 2)
+        self.X = torch.cat([roll, roll - prev], 1).to(device)
+        self.spec = (torch.rand(n, 1025, T, generator=g) * 2).pow(2).to(device)
+        self.rand_index = torch.randint(0, n, (n,), generator=g)
+        self.n = n
+
+    def __getitem__(self, i):
+        return self.X[i], self.spec[int(self.rand_index[i])], self.spec[i]
+
+    def __len__(self):
+        return self.n
+
+
+def main(args):
+    """train.py:173-208 with the synthetic dataset standing in for HDF5."""
+    hp = hyperparams(args)
+    exp_root = os.path.join(os.path.abspath('./'), 'experiments')
+    os.makedirs(exp_root, exist_ok=True)
+    exp_dir = os.path.join(exp_root, hp.exp_name)
+    os.makedirs(exp_dir, exist_ok=True)
+    model = PerformanceNet().cuda()
+    optimizer = make_optimizer(model, lr=1e-3)
+    model.zero_grad()
+    optimizer.zero_grad()
+    scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, 'min')
+    T = args.frames
+    train_ds = SyntheticSpectrogramDataset(args.n_train_read or 32, T=T, seed=1)
+    test_ds = SyntheticSpectrogramDataset(args.n_test_read or 8, T=T, seed=2)
+    train_loader = torch.utils.data.DataLoader(train_ds, batch_size=args.batch_size, shuffle=True)
+    test_loader = torch.utils.data.DataLoader(test_ds, batch_size=args.batch_size)
+    print('start training')
+    for epoch in range(hp.train_epoch):
+        loss = train(model, epoch, train_loader, optimizer, hp.iter_train_loss)
+        hp.loss_history.append(loss.item())
+        if epoch % hp.test_freq == 0:
+            test_loss = test(model, epoch, test_loader, scheduler, hp.iter_test_loss)
+            hp.test_loss_history.append(test_loss.item())
+            if test_loss < hp.best_loss:
+                print("saving model")
+                torch.save({'epoch': epoch + 1, 'state_dict': model.state_dict(),
+                            'optimizer': optimizer.state_dict()},
+                           os.path.join(exp_dir, 'checkpoint-{}.tar'.format(str(epoch + 1))))
+                hp.best_loss = test_loss.item()
+                hp.best_epoch = epoch + 1
+                with open(os.path.join(exp_dir, 'hyperparams.json'), 'w') as outfile:
+                    json.dump(hp.__dict__, outfile)
+    return hp
+
+
+def parse_args(argv=None):
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-data-dir", type=str, default='', help="(HDF5 path; synthetic data here)")
+    parser.add_argument("-epochs", type=int, default=1)
+    parser.add_argument("-test-freq", type=int, default=1)
+    parser.add_argument("-exp-name", type=str, default='piano_test')
+    parser.add_argument("--n-train-read", type=int, default=None)
+    parser.add_argument("--n-test-read", type=int, default=None)
+    parser.add_argument("--batch-size", type=int, default=16)
+    parser.add_argument("--frames", type=int, default=252)
+    return parser.parse_args(argv)
+
+
+if __name__ == "__main__":
+    main(parse_args())
+
+
+__all__ = ["train", "test", "Adam", "make_optimizer", "hyperparams", "main", "np"]

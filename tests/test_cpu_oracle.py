@@ -1,0 +1,240 @@
+"""CPU suite: the oracle against the reference's golden vectors, the C ABI surface, host logic.
+
+No compute call reaches the GPU here. The oracle (oracle/) is pinned to the reference by the
+fixtures in tests/golden (made by importing /root/reference/model/model.py); the spectral
+restatement is cross-checked against torch.stft/istft (an independent pocketfft path).
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import detinit, midi_ref
+from oracle import model_ref as R
+from oracle import spectral_ref as SR
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+# ------------------------------------------------------------- model oracle
+def test_param_names_and_shapes_match_reference():
+    g = np.load(os.path.join(GOLD, "full_B2_T44.npz"))
+    assert [n for n, _ in R.param_shapes()] == list(g["param_names"])
+    from ml_music_style_transfer_amd.model import PerformanceNet
+    net = PerformanceNet()
+    assert [(n, tuple(p.shape)) for n, p in net.named_parameters()] == R.param_shapes()
+    assert sum(p.numel() for p in net.parameters()) == 731945857  # SURVEY 6 [measured]
+    assert sum(p.numel() for n, p in net.named_parameters() if not n.startswith("MBR")) == 726039425
+
+
+def test_oracle_model_matches_reference_golden():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = np.load(os.path.join(GOLD, "full_B2_T44.npz"))
+    p = R.det_params()
+    for v in p.values():
+        v.requires_grad_(True)
+    xm, xa, cd, tg = (torch.from_numpy(a) for a in detinit.model_inputs(2, 44))
+    y = R.forward(p, xm, xa, cd)
+    loss = R.l1_loss(y, tg)
+    loss.backward()
+    assert abs(loss.item() - float(g["loss"])) <= 1e-6 * float(g["loss"])
+    yv = y.detach().double().numpy().ravel()
+    np.testing.assert_allclose(yv[g["out_idx"]], g["out_val"], rtol=1e-5, atol=1e-5)
+    for n, _ in R.param_shapes():
+        if f"gnone:{n}" in g.files:
+            assert p[n].grad is None, n
+            continue
+        gv = p[n].grad.double().numpy().ravel()[g[f"gidx:{n}"]]
+        ref = g[f"gval:{n}"]
+        assert np.abs(gv - ref).max() <= 1e-4 * max(np.abs(ref).max(), 1e-12), n
+
+
+def test_oracle_blocks_match_reference_golden():
+    g = np.load(os.path.join(GOLD, "blocks.npz"))
+    up = torch.from_numpy(g["crop:up"])
+    for d in range(-3, 4):
+        byp = torch.from_numpy(g[f"crop:d{d}:byp"])
+        out = torch.cat((up, R.crop(byp, up.shape[2])), 1)
+        np.testing.assert_array_equal(out.numpy(), g[f"crop:d{d}:out"])
+    for pool in (True, False):
+        k = f"downconv_pool{int(pool)}"
+        prm = {f"b.{n}": torch.from_numpy(detinit.param_value(n, s, 3))
+               for n, s in (("conv1.weight", (7, 5, 3)), ("conv1.bias", (7,)),
+                            ("conv2.weight", (7, 7, 3)), ("conv2.bias", (7,)))}
+        y, before = R.downconv(prm, "b", torch.from_numpy(g[k + ":x"]), pool)
+        np.testing.assert_allclose(y.numpy(), g[k + ":y"], atol=1e-6)
+        np.testing.assert_allclose(before.numpy(), g[k + ":before"], atol=1e-6)
+    x = torch.from_numpy(g["mbr:x"])
+    np.testing.assert_array_equal(g["mbr:y"], (2 * x).numpy())  # MBRBlock == 2x (model.py:172)
+    assert bool(g["mbr:conv_grads_none"])
+
+
+def test_output_length_rule():
+    # decoder output length 16*floor(T/16)+12: T = 12 (mod 16) round-trips
+    for T in (44, 60, 252, 860):
+        assert R.out_len(T) == T
+    assert R.out_len(256) == 268 and R.out_len(251) == 252
+
+
+# ---------------------------------------------------------- spectral oracle
+def test_spectral_oracle_vs_torch_stft():
+    rng = np.random.RandomState(0)
+    y = rng.randn(10000).astype(np.float32)
+    X = SR.stft(y, out_dtype=None)
+    Xt = torch.stft(torch.from_numpy(y).double(), 2048, 256, window=torch.hann_window(2048, periodic=True,
+                    dtype=torch.float64), center=True, pad_mode="reflect", return_complex=True).numpy()
+    assert X.shape == (1025, 1 + 10000 // 256)
+    np.testing.assert_allclose(X, Xt, atol=1e-9)
+    yi = SR.istft(X)
+    yt = torch.istft(torch.from_numpy(Xt), 2048, 256, window=torch.hann_window(2048, periodic=True,
+                     dtype=torch.float64), center=True, length=256 * (X.shape[1] - 1)).numpy()
+    np.testing.assert_allclose(yi, yt, atol=1e-9)
+    np.testing.assert_allclose(yi, y[:yi.size], atol=1e-5)
+    lp = SR.logpow(y)
+    assert lp.dtype == np.float32 and lp.shape == X.shape
+
+
+def test_mel_filter_properties():
+    w = SR.mel_filter(16000)
+    assert w.shape == (128, 1025) and w.dtype == np.float32
+    assert (w >= 0).all() and (w.sum(1) > 0).all()
+    # slaney area normalisation: each triangle integrates (over Hz) to ~1
+    df = 16000 / 2048
+    area = w.sum(1) * df
+    assert np.all(np.abs(area[10:] - 1) < 0.1)
+    # every bin feeds at most two bands
+    assert ((w > 0).sum(0) <= 2).all()
+    from ml_music_style_transfer_amd import spectral
+    np.testing.assert_allclose(spectral.mel_basis(16000), w, rtol=1e-6, atol=1e-9)
+
+
+def test_griffinlim_oracle_converges():
+    rng = np.random.RandomState(1)
+    t = np.arange(256 * 40) / 16000
+    y = (0.3 * np.sin(2 * np.pi * 440 * t) + 0.1 * np.sin(2 * np.pi * 1100 * t)).astype(np.float32)
+    S = np.abs(SR.stft(y, out_dtype=None))
+    ang = np.exp(2j * np.pi * rng.rand(*S.shape))
+    y1 = SR.griffinlim(S, n_iter=1, angles=ang)
+    y30 = SR.griffinlim(S, n_iter=30, angles=ang)
+    sc = lambda z: np.linalg.norm(np.abs(SR.stft(z, out_dtype=None)) - S) / np.linalg.norm(S)  # noqa
+    assert sc(y30) < 0.5 * sc(y1)
+
+
+# ------------------------------------------------------- framing / midi rules
+def test_framing_constants_and_chunks():
+    hp = midi_ref.Hyper()
+    assert hp.wps == 172  # 44100 // 256 (preprocess.py:41)
+    s, e = midi_ref.audio_chunk_bounds(hp, 0)
+    assert e - s == 219904 and 1 + (e - s) // hp.ws == 860  # T = 860 frames
+    assert midi_ref.audio_chunk_bounds(hp, 2)[0] == 2 * 256 * 512
+    assert midi_ref.roll_chunk_bounds(hp, 3) == (1536, 1536 + 860)
+    assert midi_ref.num_song_chunks(860 + 512 * 30 + 7, hp) == 30 - 3
+    assert midi_ref.num_song_chunks(100000, hp) == 100
+    hp16 = midi_ref.Hyper(sr=16000)
+    assert hp16.wps == 62
+    from ml_music_style_transfer_amd import preprocess as PP
+    assert PP.chunk_bounds_audio(2) == midi_ref.audio_chunk_bounds(hp, 2)
+    assert PP.chunk_bounds_roll(3) == midi_ref.roll_chunk_bounds(hp, 3)
+    assert PP.get_num_song_chunks(np.zeros((860 + 512 * 30 + 7, 128))) == 27
+
+
+def test_onoff_rule_is_frame_difference():
+    rng = np.random.RandomState(2)
+    roll = (rng.rand(200, 128) < 0.05) * rng.randint(1, 127, (200, 128))
+    b, o = midi_ref.binarize_and_onoff(roll.astype(np.float64))
+    prev = np.vstack([np.zeros((1, 128)), b[:-1]])
+    np.testing.assert_array_equal(o, b - prev)
+    item = midi_ref.assemble_item(b[:44], o[:44])
+    assert item.shape == (256, 44)
+    from ml_music_style_transfer_amd import preprocess as PP
+    notes = [(60, 0.1, 0.5, 80), (64, 0.25, 0.3, 90)]
+    np.testing.assert_array_equal(PP.piano_roll_from_notes(notes, 62),
+                                  midi_ref.piano_roll(notes, 62))
+
+
+# -------------------------------------------------------------- C ABI surface
+def _header_symbols():
+    text = open(os.path.join(ROOT, "include", "mst.h")).read()
+    return sorted(set(re.findall(r"\b(mst_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    from ml_music_style_transfer_amd import _lib as L
+    lib = L.load()
+    syms = _header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(L.SIGNATURES) == syms
+    assert lib.mst_version().startswith(b"libmst_hip")
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (mst_\w+)", out))
+    assert set(syms) <= exported
+
+
+def test_ctypes_struct_layout_matches_c(tmp_path):
+    from ml_music_style_transfer_amd import _lib as L
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mst.h"\n'
+                   'int main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(mst_src),'
+                   ' sizeof(mst_dst), sizeof(mst_conv_desc), sizeof(mst_wgrad_desc),'
+                   ' offsetof(mst_conv_desc, dst), offsetof(mst_conv_desc, seed),'
+                   ' offsetof(mst_wgrad_desc, out), offsetof(mst_wgrad_desc, src)); return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    c = [int(v) for v in subprocess.check_output([str(exe)]).split()]
+    py = [ctypes.sizeof(L.MstSrc), ctypes.sizeof(L.MstDst), ctypes.sizeof(L.MstConvDesc),
+          ctypes.sizeof(L.MstWgradDesc), L.MstConvDesc.dst.offset, L.MstConvDesc.seed.offset,
+          L.MstWgradDesc.out.offset, L.MstWgradDesc.src.offset]
+    assert c == py
+
+
+def test_product_path_has_no_cpu_fallback():
+    from ml_music_style_transfer_amd.model import PerformanceNet, DownConv
+    from ml_music_style_transfer_amd import spectral
+    with pytest.raises(RuntimeError):
+        DownConv(4, 8, 0)(torch.zeros(1, 4, 12))
+    with pytest.raises(RuntimeError):
+        spectral.stft_logpow(torch.zeros(4096))
+    del PerformanceNet
+
+
+def test_product_package_never_imports_oracle():
+    pkg = os.path.join(ROOT, "ml_music_style_transfer_amd")
+    for dp, _, fs in os.walk(pkg):
+        for f in fs:
+            if f.endswith((".py", ".hip", ".h")):
+                text = open(os.path.join(dp, f)).read()
+                assert "oracle" not in re.sub(r"#.*|//.*", "", text).replace('"""', ""), f
+
+
+# ----------------------------------------------------------------- host logic
+def test_crop_offset_semantics():
+    from ml_music_style_transfer_amd import engine as E
+    g = np.load(os.path.join(GOLD, "blocks.npz"))
+    up = g["crop:up"]
+    for d in range(-3, 4):
+        byp = g[f"crop:d{d}:byp"]
+        c = E.crop_offset(byp.shape[2], up.shape[2])
+        ref = g[f"crop:d{d}:out"][:, up.shape[1]:]
+        for t in range(up.shape[2]):
+            s = t + c
+            want = byp[:, :, s] if 0 <= s < byp.shape[2] else 0
+            np.testing.assert_array_equal(ref[:, :, t], want)
+
+
+def test_convT_lengths_and_subpixel_taps():
+    from ml_music_style_transfer_amd import kernels as K
+    for k, tin in ((6, 15), (4, 32), (3, 64), (2, 127)):
+        tout = K.convT2_out_len(tin, k)
+        assert tout == torch.nn.functional.conv_transpose1d(
+            torch.zeros(1, 1, tin), torch.zeros(1, 1, k), stride=2, padding=1).shape[2]
+        # the two phases cover every output exactly once with k taps in total
+        nq = [k // 2, (k + 1) // 2]
+        assert sum(nq) == k
+        assert (tout + 1) // 2 + tout // 2 == tout
