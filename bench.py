@@ -192,12 +192,12 @@ def main():
         step()
     K.gemm_timing(None)
     torch.cuda.synchronize()
-    gemm_ms = sum(s.elapsed_time(e) for s, e, _, _ in log)
-    gemm_flops = sum(f for _, _, f, _ in log)
+    gemm_ms = sum(ev[0].elapsed_time(ev[1]) for ev in log)
+    gemm_flops = sum(ev[2] for ev in log)
     n_steps_t = max(1, args.kernel_timing_steps)
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     by_tag = {}
-    for s, e, f, tag in log:
+    for s, e, f, tag, _ in log:
         a = by_tag.setdefault(tag, [0.0, 0.0, 0])
         a[0] += s.elapsed_time(e)
         a[1] += f

@@ -29,7 +29,7 @@ struct GP {
   // conv A operand
   const float* A;
   long long sAm, sAc, sAt;
-  int a_vec;
+  int a_mode;  // 0: k-scalar, 1: k-vector (float4), 2: m-major
   // wgrad A operand (P = dY or X, time contiguous)
   const float* P;
   long long sPb;
@@ -78,18 +78,21 @@ __device__ __forceinline__ void divmod_f(int k, int d, float inv, int& q, int& r
   else if (r >= d) { ++q; r -= d; }
 }
 
-// X(b, c, tin) of the virtual concatenated input, zero outside its valid ranges.
-__device__ __forceinline__ float load_x(const GP& p, const float* base0, const float* base1, int c,
-                                        int tin) {
-  if ((unsigned)tin >= (unsigned)p.Tv) return 0.f;
-  if (c < p.C0) {
-    int ts = tin + p.off0;
-    if ((unsigned)ts >= (unsigned)p.T0) return 0.f;
-    return base0[(long long)c * p.sc0 + ts];
-  }
-  int ts = tin + p.off1;
-  if ((unsigned)ts >= (unsigned)p.T1) return 0.f;
-  return base1[(long long)(c - p.C0) * p.sc1 + ts];
+// Out-of-range operand elements (padding, tails, crop) are loaded from this zero block
+// instead of being predicated: loads stay branch-free AND need no select after the load, so
+// the prefetch of tile k+1 stays in flight across tile k's MFMAs (a per-element
+// `ok ? v : 0` right after the load made hipcc wait vmcnt(0) before the compute).
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+
+// Address of X(b, c, tin) of the virtual concatenated input, or of a zero when outside
+// its valid ranges.
+__device__ __forceinline__ const float* addr_x(const GP& p, const float* base0,
+                                               const float* base1, int c, int tin, bool ok) {
+  const bool s1 = c >= p.C0;
+  const int ts = tin + (s1 ? p.off1 : p.off0);
+  ok = ok && ((unsigned)tin < (unsigned)p.Tv) && ((unsigned)ts < (unsigned)(s1 ? p.T1 : p.T0));
+  const float* ptr = s1 ? base1 + (long long)(c - p.C0) * p.sc1 : base0 + (long long)c * p.sc0;
+  return ok ? ptr + ts : g_zero4;
 }
 
 __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
@@ -129,7 +132,7 @@ __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) 
   *o = v;
 }
 
-template <int TAPS, bool WG>
+template <int TAPS, bool WG, int AMODE>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
 
@@ -144,29 +147,29 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
 
   // ---- per-thread loader coordinates ----
-  // A tile units: rows ma = (tid>>3) + 32u (u=0..3), k quad = tid&7
-  const int akq = (tid & 7) * 4;
-  // B tile units: column nb = tid & 127, k quads (tid>>7) + 2u
-  const int nbl = tid & 127;
-  const int nb = n0 + nbl;
-  const bool nb_ok = nb < p.N;
-  const int bkq0 = (tid >> 7);
+  // Two unit mappings of a 128-row x 32-k tile onto 256 threads, 4 units of 4 consecutive k:
+  //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7   -> 8 lanes run along k
+  //   RM ("row-major"): row = tid&127, k quads (tid>>7) + 2u -> lanes run along rows
+  // Both store a unit as one conflict-free ds_write_b128 into the [row][k] LDS image.
+  // A: AMODE 0/1 (k-scalar / k-vector) use KM, AMODE 2 (m contiguous in memory) uses RM.
+  // B: conv/dgrad (n = time, contiguous) use RM; wgrad (k = time) uses KM.
+  const int km_row = tid >> 3;
+  const int km_kq = (tid & 7) * 4;
+  const int rm_row = tid & 127;
+  const int rm_kq0 = tid >> 7;
 
-  // conv B: n -> (b, t) fixed per thread
+  // conv B (RM): n -> (b, t) fixed per thread
+  const int nb = n0 + rm_row;
+  const bool nb_ok = nb < p.N;
   const float* xb0 = nullptr;
   const float* xb1 = nullptr;
   int tbase = 0;
-  // wgrad B: n -> (c, tap) fixed per thread
-  int wc = 0, wtap = 0;
   if constexpr (!WG) {
     int bb = nb_ok ? nb / p.Tn : 0;
     int tt = nb_ok ? nb - bb * p.Tn : 0;
     tbase = p.ta * tt + p.tb;
     xb0 = p.x0 + (long long)bb * p.sb0;
-    xb1 = p.x1 ? p.x1 + (long long)bb * p.sb1 : nullptr;
-  } else {
-    wc = nb / TAPS;
-    wtap = nb - wc * TAPS;
+    xb1 = p.x1 + (long long)bb * p.sb1;  // never dereferenced when there is no second source
   }
 
   float ra[4][4], rb[4][4];
@@ -175,19 +178,20 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     const int k0 = kt * BK;
     // ---------------- A ----------------
     if constexpr (!WG) {
-      const int kk = k0 + akq;
-      if (p.a_vec) {
+      if constexpr (AMODE == 1) {
+        const int kk = k0 + km_kq;
+        const bool kok = kk < p.K;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          int m = m0 + (tid >> 3) + 32 * u;
-          if (m < p.M && kk < p.K) {
-            f32x4 v = *reinterpret_cast<const f32x4*>(p.A + (long long)m * p.sAm + kk);
-            ra[u][0] = v[0]; ra[u][1] = v[1]; ra[u][2] = v[2]; ra[u][3] = v[3];
-          } else {
-            ra[u][0] = ra[u][1] = ra[u][2] = ra[u][3] = 0.f;
-          }
+          const int m = m0 + km_row + 32 * u;
+          const bool ok = kok && m < p.M;
+          const f32x4 v =
+              *reinterpret_cast<const f32x4*>(ok ? p.A + (long long)m * p.sAm + kk : g_zero4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ra[u][i] = v[i];
         }
-      } else {
+      } else if constexpr (AMODE == 0) {
+        const int kk = k0 + km_kq;
         long long koff[4];
         bool kok[4];
 #pragma unroll
@@ -200,15 +204,33 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          int m = m0 + (tid >> 3) + 32 * u;
-          const float* ar = p.A + (long long)m * p.sAm;
+          const int m = m0 + km_row + 32 * u;
+          const long long mo = (long long)m * p.sAm;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[u][i] = (m < p.M && kok[i]) ? ar[koff[i]] : 0.f;
+          for (int i = 0; i < 4; ++i) {
+            const bool ok = kok[i] && m < p.M;
+            ra[u][i] = *(ok ? p.A + mo + koff[i] : g_zero4);
+          }
+        }
+      } else {  // AMODE 2: lanes along m (small |sAm|, e.g. transposed weight reads in dgrad)
+        const int m = m0 + rm_row;
+        const long long mo = (long long)m * p.sAm;
+        const bool mok = m < p.M;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int k = k0 + (rm_kq0 + 2 * u) * 4 + i;
+            const int c = k / TAPS;
+            const int tap = k - c * TAPS;
+            const bool ok = mok && k < p.K;
+            ra[u][i] = *(ok ? p.A + mo + (long long)c * p.sAc + (long long)tap * p.sAt : g_zero4);
+          }
         }
       }
     } else {
-      // A(m, k) = P[b][m][t], (b, t) = divmod(k, Tk)
-      const int k = k0 + akq;
+      // A(m, k) = P[b][m][t], (b, t) = divmod(k, Tk)   (KM: lanes along t)
+      const int k = k0 + km_kq;
       long long off[4];
       bool ok[4];
 #pragma unroll
@@ -220,42 +242,50 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        int m = m0 + (tid >> 3) + 32 * u;
-        const float* pr = p.P + (long long)m * p.sPc;
+        const int m = m0 + km_row + 32 * u;
+        const long long mo = (long long)m * p.sPc;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[u][i] = (m < p.M && ok[i]) ? pr[off[i]] : 0.f;
+        for (int i = 0; i < 4; ++i) {
+          const bool okm = ok[i] && m < p.M;
+          ra[u][i] = *(okm ? p.P + mo + off[i] : g_zero4);
+        }
       }
     }
     // ---------------- B ----------------
     if constexpr (!WG) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        int kq = (bkq0 + 2 * u) * 4;
+        int kq = (rm_kq0 + 2 * u) * 4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           int k = k0 + kq + i;
           int c = k / TAPS;
           int tap = k - c * TAPS;
-          float v = 0.f;
-          if (nb_ok && k < p.K) v = load_x(p, xb0, xb1, c, tbase + p.tg * tap);
-          rb[u][i] = v;
+          rb[u][i] = *addr_x(p, xb0, xb1, c, tbase + p.tg * tap, nb_ok && k < p.K);
         }
       }
     } else {
+      // B(k=(b,t), n=(c,tap)) = X[b][c][a*t + beta + g*tap]   (KM: lanes along t)
+      const int k = k0 + km_kq;
+      int bs[4], ts[4];
+      bool kok[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        divmod_f(k + i, p.Tk, p.invTk, bs[i], ts[i]);
+        kok[i] = (k + i) < p.K;
+        bs[i] = kok[i] ? bs[i] : 0;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int k = k0 + (bkq0 + 2 * u) * 4;
+        const int n = n0 + km_row + 32 * u;
+        const int c = n / TAPS;
+        const int tap = n - c * TAPS;
+        const bool nok = n < p.N;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          int b, t;
-          divmod_f(k + i, p.Tk, p.invTk, b, t);
-          float v = 0.f;
-          if (nb_ok && (k + i) < p.K) {
-            const float* base0 = p.x0 + (long long)b * p.sb0;
-            const float* base1 = p.x1 ? p.x1 + (long long)b * p.sb1 : nullptr;
-            v = load_x(p, base0, base1, wc, p.ta * t + p.tb + p.tg * wtap);
-          }
-          rb[u][i] = v;
+          const float* base0 = p.x0 + (long long)bs[i] * p.sb0;
+          const float* base1 = p.x1 + (long long)bs[i] * p.sb1;
+          rb[u][i] = *addr_x(p, base0, base1, c, p.ta * ts[i] + p.tb + p.tg * tap, nok && kok[i]);
         }
       }
     }
@@ -266,15 +296,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     float* Bs = lds[buf] + BM * LDK;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      int ml = (tid >> 3) + 32 * u;
       f32x4 v = {ra[u][0], ra[u][1], ra[u][2], ra[u][3]};
-      *reinterpret_cast<f32x4*>(As + ml * LDK + akq) = v;
+      if constexpr (AMODE == 2 && !WG)
+        *reinterpret_cast<f32x4*>(As + rm_row * LDK + (rm_kq0 + 2 * u) * 4) = v;
+      else
+        *reinterpret_cast<f32x4*>(As + (km_row + 32 * u) * LDK + km_kq) = v;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      int kq = (bkq0 + 2 * u) * 4;
       f32x4 v = {rb[u][0], rb[u][1], rb[u][2], rb[u][3]};
-      *reinterpret_cast<f32x4*>(Bs + nbl * LDK + kq) = v;
+      if constexpr (WG)
+        *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
+      else
+        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + (rm_kq0 + 2 * u) * 4) = v;
     }
   };
 
@@ -289,14 +323,16 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int r32 = lane & 31;
   const int h = lane >> 5;
 
+  // Branch-free main loop: the prefetch of tile k+1 is issued unconditionally (past the
+  // end of K every element resolves to the zero block) so no control-flow join forces a
+  // vmcnt(0) between the prefetch and this tile's MFMAs.
   if (kt0 < kt1) {
     load_tile(kt0);
     store_tile(0);
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
       const int buf = (kt - kt0) & 1;
-      const bool more = kt + 1 < kt1;
-      if (more) load_tile(kt + 1);
+      load_tile(kt + 1);
       const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
       const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
 #pragma unroll
@@ -313,7 +349,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
           acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
         }
       }
-      if (more) store_tile(buf ^ 1);
+      store_tile(buf ^ 1);
       __syncthreads();
     }
   }
@@ -368,9 +404,9 @@ int choose_splitk(int M, int N, int nk, int req) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
   long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
   const long long target = 512;  // two workgroups per CU on 256 CUs
-  if (tiles >= 192 || nk < 8) return 1;
+  if (tiles >= 384 || nk < 16) return 1;
   int s = (int)((target + tiles - 1) / tiles);
-  int maxs = nk / 4;  // at least four K tiles per split
+  int maxs = nk / 8;  // at least eight K tiles per split
   if (s > maxs) s = maxs;
   if (s > 32) s = 32;
   return s < 1 ? 1 : s;
@@ -380,8 +416,15 @@ template <bool WG>
 int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   dim3 block(NTHR);
-#define MST_GEMM_CASE(TP) \
-  case TP: hipLaunchKernelGGL((gemm_kernel<TP, WG>), grid, block, 0, st, p); break;
+#define MST_GEMM_CASE(TP)                                                             \
+  case TP:                                                                            \
+    if (WG || p.a_mode == 0)                                                          \
+      hipLaunchKernelGGL((gemm_kernel<TP, WG, 0>), grid, block, 0, st, p);            \
+    else if (p.a_mode == 1)                                                           \
+      hipLaunchKernelGGL((gemm_kernel<TP, WG, (WG ? 0 : 1)>), grid, block, 0, st, p); \
+    else                                                                              \
+      hipLaunchKernelGGL((gemm_kernel<TP, WG, (WG ? 0 : 2)>), grid, block, 0, st, p); \
+    break;
   switch (taps) {
     MST_GEMM_CASE(1)
     MST_GEMM_CASE(2)
@@ -435,8 +478,10 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.sAm = d->sAm;
   p.sAc = d->sAc;
   p.sAt = d->sAt;
-  p.a_vec = (d->sAt == 1 && d->sAc == d->taps && (d->sAm % 4) == 0 && (p.K % 4) == 0 &&
-             ((uintptr_t)d->A % 16) == 0);
+  const bool kvec = d->sAt == 1 && d->sAc == d->taps && (d->sAm % 4) == 0 && (p.K % 4) == 0 &&
+                    ((uintptr_t)d->A % 16) == 0;
+  const long long am = d->sAm < 0 ? -d->sAm : d->sAm;
+  p.a_mode = kvec ? 1 : (am <= 8 ? 2 : 0);
   fill_src(p, d->src, d->Ctot);
   p.Tv = d->Tv;
   p.ta = d->a;

@@ -83,7 +83,7 @@ def gemm_timing(log):
     _GEMM_LOG = log
 
 
-def _timed(launch, flops, tag):
+def _timed(launch, flops, tag, shape=None):
     if _GEMM_LOG is None:
         launch()
         return
@@ -92,7 +92,7 @@ def _timed(launch, flops, tag):
     s.record()
     launch()
     e.record()
-    _GEMM_LOG.append((s, e, flops, tag))
+    _GEMM_LOG.append((s, e, flops, tag, shape))
 
 
 def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt, dsts, ostride=1,
@@ -118,7 +118,7 @@ def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt
     ref = ctypes.byref(d)
     ws, nb = _workspace(lib.mst_conv_fwd_workspace_size(ref), A.device)
     _timed(lambda: L.check(lib.mst_conv_fwd_f32(ref, L.ptr(ws), nb, L.stream()), "mst_conv_fwd_f32"),
-           2.0 * M * B * Tn * d.Ctot * taps, "conv")
+           2.0 * M * B * Tn * d.Ctot * taps, "conv", (M, B * Tn, d.Ctot * taps, taps, a, nb))
 
 
 def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate=False, splitk=0):
@@ -141,7 +141,8 @@ def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate
     ref = ctypes.byref(d)
     ws, nb = _workspace(lib.mst_wgrad_workspace_size(ref), P.device)
     _timed(lambda: L.check(lib.mst_conv_wgrad_f32(ref, L.ptr(ws), nb, L.stream()),
-                           "mst_conv_wgrad_f32"), 2.0 * M * B * Tk * d.Ctot * taps, "wgrad")
+                           "mst_conv_wgrad_f32"), 2.0 * M * B * Tk * d.Ctot * taps, "wgrad",
+           (M, d.Ctot * taps, B * Tk, taps, a, nb))
 
 
 # ---------------------------------------------------------------- Conv1d k3 p1
