@@ -18,14 +18,27 @@
 // register-staged prefetch (global loads of tile k+1 in flight during tile k's MFMAs).
 // Lane half h = lane>>5 owns k in [16h, 16h+16) of each BK tile, so one ds_read_b128
 // gives a lane four consecutive MFMA k-steps.
+//
+// Operands are fetched with raw buffer loads (32-bit byte offsets into a descriptor per
+// tensor): an element outside the tensor's valid ranges gets an out-of-range offset and the
+// hardware returns 0, so the loaders have no branches and no post-load selects. fp32 MFMA
+// shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
+// every loader VALU instruction costs MFMA issue time: the per-element index work is kept
+// wave-uniform (scalar) wherever the mapping allows it.
 #include "common.h"
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256, LDK = BK + 4;
 
+constexpr uint32_t OOB = 0x7FFFFFF0u;  // byte offset past every descriptor's num_records
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
 struct GP {
   int M, N, K, nk, splitk;
+  long long nA, nP, nx0, nx1;  // elements addressable through each operand descriptor
+  int dual;                    // second input source present
   // conv A operand
   const float* A;
   long long sAm, sAc, sAt;
@@ -41,7 +54,7 @@ struct GP {
   int sc0, C0, T0, off0;
   const float* x1;
   long long sb1;
-  int sc1, T1, off1;
+  int sc1, T1, off1, C1;
   int Tv, ta, tb, tg;
   int Tn;
   // conv epilogue
@@ -76,23 +89,6 @@ __device__ __forceinline__ void divmod_f(int k, int d, float inv, int& q, int& r
   r = k - q * d;
   if (r < 0) { --q; r += d; }
   else if (r >= d) { ++q; r -= d; }
-}
-
-// Out-of-range operand elements (padding, tails, crop) are loaded from this zero block
-// instead of being predicated: loads stay branch-free AND need no select after the load, so
-// the prefetch of tile k+1 stays in flight across tile k's MFMAs (a per-element
-// `ok ? v : 0` right after the load made hipcc wait vmcnt(0) before the compute).
-__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
-
-// Address of X(b, c, tin) of the virtual concatenated input, or of a zero when outside
-// its valid ranges.
-__device__ __forceinline__ const float* addr_x(const GP& p, const float* base0,
-                                               const float* base1, int c, int tin, bool ok) {
-  const bool s1 = c >= p.C0;
-  const int ts = tin + (s1 ? p.off1 : p.off0);
-  ok = ok && ((unsigned)tin < (unsigned)p.Tv) && ((unsigned)ts < (unsigned)(s1 ? p.T1 : p.T0));
-  const float* ptr = s1 ? base1 + (long long)(c - p.C0) * p.sc1 : base0 + (long long)c * p.sc0;
-  return ok ? ptr + ts : g_zero4;
 }
 
 __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
@@ -132,7 +128,19 @@ __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) 
   *o = v;
 }
 
-template <int TAPS, bool WG, int AMODE>
+__device__ __forceinline__ rsrc_t mk_rsrc(const float* ptr, long long n) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)ptr, (short)0, (int)(n * 4), 0x00020000);
+}
+
+__device__ __forceinline__ float ldb(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0));
+}
+
+__device__ __forceinline__ f32x4 ldb4(rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
+}
+
+template <int TAPS, bool WG, int AMODE, bool DUAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
 
@@ -146,148 +154,154 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int kt0 = (int)((long long)split * p.nk / p.splitk);
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
 
-  // ---- per-thread loader coordinates ----
   // Two unit mappings of a 128-row x 32-k tile onto 256 threads, 4 units of 4 consecutive k:
-  //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7   -> 8 lanes run along k
-  //   RM ("row-major"): row = tid&127, k quads (tid>>7) + 2u -> lanes run along rows
+  //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7 -> 8 lanes run along k
+  //   RM ("row-major"): row = tid&127, k quads kw + 2u    -> lanes run along rows; k is
+  //                     wave-uniform (kw = tid>>7 via readfirstlane), so its decode is scalar
   // Both store a unit as one conflict-free ds_write_b128 into the [row][k] LDS image.
-  // A: AMODE 0/1 (k-scalar / k-vector) use KM, AMODE 2 (m contiguous in memory) uses RM.
-  // B: conv/dgrad (n = time, contiguous) use RM; wgrad (k = time) uses KM.
+  // A: AMODE 1 (k-contiguous, float4) and 0 (k-scalar) use KM; AMODE 2 (m-contiguous) RM.
+  // B: conv/dgrad (n = time, contiguous) RM; wgrad (k = time) KM.
   const int km_row = tid >> 3;
   const int km_kq = (tid & 7) * 4;
   const int rm_row = tid & 127;
-  const int rm_kq0 = tid >> 7;
-
-  // conv B (RM): n -> (b, t) fixed per thread
-  const int nb = n0 + rm_row;
-  const bool nb_ok = nb < p.N;
-  const float* xb0 = nullptr;
-  const float* xb1 = nullptr;
-  int tbase = 0;
-  if constexpr (!WG) {
-    int bb = nb_ok ? nb / p.Tn : 0;
-    int tt = nb_ok ? nb - bb * p.Tn : 0;
-    tbase = p.ta * tt + p.tb;
-    xb0 = p.x0 + (long long)bb * p.sb0;
-    xb1 = p.x1 + (long long)bb * p.sb1;  // never dereferenced when there is no second source
-  }
+  const int kw = __builtin_amdgcn_readfirstlane(tid >> 7);
 
   float ra[4][4], rb[4][4];
 
+  // ------------------------------------------------------------ loaders
+  const rsrc_t rX0 = mk_rsrc(p.x0, p.nx0);
+  const rsrc_t rX1 = mk_rsrc(DUAL ? p.x1 : p.x0, DUAL ? p.nx1 : 0);
+  const rsrc_t rA = mk_rsrc(WG ? p.P : p.A, WG ? p.nP : p.nA);
+
+  // per-lane constants
+  uint32_t rowA[4];
+  int tinb = 0;
+  uint32_t colb0 = 0, colb1 = 0;
+  // wgrad B rows
+  uint32_t rowX[4];
+  int gtb[4], offs[4], Tsrc[4];
+  bool nsel1[4];
+  if constexpr (!WG) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = m0 + (AMODE == 2 ? rm_row : km_row + 32 * u);
+      rowA[u] = m < p.M ? (uint32_t)(m * p.sAm) * 4u : OOB;
+    }
+    const int n = n0 + rm_row;
+    const int bb = n / p.Tn;
+    const int tt = n - bb * p.Tn;
+    tinb = n < p.N ? p.ta * tt + p.tb : -(1 << 29);  // invalid column: every tap out of range
+    colb0 = (uint32_t)(bb * p.sb0) * 4u;
+    colb1 = DUAL ? (uint32_t)(bb * p.sb1) * 4u : 0u;
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int m = m0 + km_row + 32 * u;
+      rowA[u] = m < p.M ? (uint32_t)(m * p.sPc) * 4u : OOB;
+      const int n = n0 + km_row + 32 * u;
+      const int c = n / TAPS;
+      const int tap = n - c * TAPS;
+      const bool s1 = DUAL && c >= p.C0;
+      nsel1[u] = s1;
+      rowX[u] = (uint32_t)(s1 ? (c - p.C0) * p.sc1 : c * p.sc0) * 4u;
+      gtb[u] = n < p.N ? p.tb + p.tg * tap : -(1 << 29);
+      offs[u] = s1 ? p.off1 : p.off0;
+      Tsrc[u] = s1 ? p.T1 : p.T0;
+    }
+  }
+
   auto load_tile = [&](int kt) {
     const int k0 = kt * BK;
-    // ---------------- A ----------------
     if constexpr (!WG) {
+      // ---------------- A ----------------
       if constexpr (AMODE == 1) {
-        const int kk = k0 + km_kq;
-        const bool kok = kk < p.K;
+        const int k = k0 + km_kq;
+        const uint32_t kb = k < p.K ? (uint32_t)k * 4u : OOB;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int m = m0 + km_row + 32 * u;
-          const bool ok = kok && m < p.M;
-          const f32x4 v =
-              *reinterpret_cast<const f32x4*>(ok ? p.A + (long long)m * p.sAm + kk : g_zero4);
+          const f32x4 v = ldb4(rA, rowA[u] + kb);
 #pragma unroll
           for (int i = 0; i < 4; ++i) ra[u][i] = v[i];
         }
       } else if constexpr (AMODE == 0) {
-        const int kk = k0 + km_kq;
-        long long koff[4];
-        bool kok[4];
+        uint32_t koff[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          int k = kk + i;
-          int c = k / TAPS;
-          int tap = k - c * TAPS;
-          koff[i] = (long long)c * p.sAc + (long long)tap * p.sAt;
-          kok[i] = k < p.K;
+          const int k = k0 + km_kq + i;
+          const int c = k / TAPS;
+          const int tap = k - c * TAPS;
+          koff[i] = k < p.K ? (uint32_t)(c * p.sAc + tap * p.sAt) * 4u : OOB;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int m = m0 + km_row + 32 * u;
-          const long long mo = (long long)m * p.sAm;
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ra[u][i] = ldb(rA, rowA[u] + koff[i]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bool ok = kok[i] && m < p.M;
-            ra[u][i] = *(ok ? p.A + mo + koff[i] : g_zero4);
-          }
-        }
-      } else {  // AMODE 2: lanes along m (small |sAm|, e.g. transposed weight reads in dgrad)
-        const int m = m0 + rm_row;
-        const long long mo = (long long)m * p.sAm;
-        const bool mok = m < p.M;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int k = k0 + (rm_kq0 + 2 * u) * 4 + i;
+            const int k = k0 + 4 * (kw + 2 * u) + i;  // wave-uniform
             const int c = k / TAPS;
             const int tap = k - c * TAPS;
-            const bool ok = mok && k < p.K;
-            ra[u][i] = *(ok ? p.A + mo + (long long)c * p.sAc + (long long)tap * p.sAt : g_zero4);
+            const uint32_t koff = k < p.K ? (uint32_t)(c * p.sAc + tap * p.sAt) * 4u : OOB;
+            ra[u][i] = ldb(rA, rowA[0] + koff);
           }
-        }
       }
+      // ---------------- B: X(b, c, a*t + beta + g*tap), column per lane ----------------
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = k0 + 4 * (kw + 2 * u) + i;  // wave-uniform
+          const int c = k / TAPS;
+          const int tap = k - c * TAPS;
+          const bool s1 = DUAL && c >= p.C0;
+          const int off = s1 ? p.off1 : p.off0;
+          const int Ts = s1 ? p.T1 : p.T0;
+          const uint32_t cb = (uint32_t)(s1 ? (c - p.C0) * p.sc1 : c * p.sc0) * 4u;
+          const int tin = tinb + p.tg * tap;
+          const int ts = tin + off;
+          const bool ok = (k < p.K) & ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)Ts);
+          const uint32_t voff = ok ? (s1 ? colb1 : colb0) + cb + (uint32_t)ts * 4u : OOB;
+          rb[u][i] = ldb(s1 ? rX1 : rX0, voff);
+        }
     } else {
-      // A(m, k) = P[b][m][t], (b, t) = divmod(k, Tk)   (KM: lanes along t)
+      // wgrad: k = (b, t) per lane (KM)
       const int k = k0 + km_kq;
-      long long off[4];
-      bool ok[4];
+      uint32_t kP[4], kb0[4], kb1[4];
+      int ta_t[4];
+      bool kok[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int b, t;
         divmod_f(k + i, p.Tk, p.invTk, b, t);
-        ok[i] = (k + i) < p.K;
-        off[i] = (long long)b * p.sPb + t;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int m = m0 + km_row + 32 * u;
-        const long long mo = (long long)m * p.sPc;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool okm = ok[i] && m < p.M;
-          ra[u][i] = *(okm ? p.P + mo + off[i] : g_zero4);
-        }
-      }
-    }
-    // ---------------- B ----------------
-    if constexpr (!WG) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        int kq = (rm_kq0 + 2 * u) * 4;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          int k = k0 + kq + i;
-          int c = k / TAPS;
-          int tap = k - c * TAPS;
-          rb[u][i] = *addr_x(p, xb0, xb1, c, tbase + p.tg * tap, nb_ok && k < p.K);
-        }
-      }
-    } else {
-      // B(k=(b,t), n=(c,tap)) = X[b][c][a*t + beta + g*tap]   (KM: lanes along t)
-      const int k = k0 + km_kq;
-      int bs[4], ts[4];
-      bool kok[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        divmod_f(k + i, p.Tk, p.invTk, bs[i], ts[i]);
         kok[i] = (k + i) < p.K;
-        bs[i] = kok[i] ? bs[i] : 0;
+        kP[i] = kok[i] ? (uint32_t)(b * p.sPb + t) * 4u : OOB;
+        kb0[i] = (uint32_t)(b * p.sb0) * 4u;
+        kb1[i] = DUAL ? (uint32_t)(b * p.sb1) * 4u : 0u;
+        ta_t[i] = kok[i] ? p.ta * t : -(1 << 29);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int n = n0 + km_row + 32 * u;
-        const int c = n / TAPS;
-        const int tap = n - c * TAPS;
-        const bool nok = n < p.N;
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[u][i] = ldb(rA, rowA[u] + kP[i]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float* base0 = p.x0 + (long long)bs[i] * p.sb0;
-          const float* base1 = p.x1 + (long long)bs[i] * p.sb1;
-          rb[u][i] = *addr_x(p, base0, base1, c, p.ta * ts[i] + p.tb + p.tg * tap, nok && kok[i]);
+          const int tin = ta_t[i] + gtb[u];
+          const int ts = tin + offs[u];
+          const bool ok = (unsigned)tin < (unsigned)p.Tv && (unsigned)ts < (unsigned)Tsrc[u];
+          const uint32_t base = rowX[u] + (uint32_t)ts * 4u;
+          if constexpr (DUAL) {
+            const float v0 = ldb(rX0, ok && !nsel1[u] ? base + kb0[i] : OOB);
+            const float v1 = ldb(rX1, ok && nsel1[u] ? base + kb1[i] : OOB);
+            rb[u][i] = v0 + v1;
+          } else {
+            rb[u][i] = ldb(rX0, ok ? base + kb0[i] : OOB);
+          }
         }
-      }
     }
   };
 
@@ -298,7 +312,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     for (int u = 0; u < 4; ++u) {
       f32x4 v = {ra[u][0], ra[u][1], ra[u][2], ra[u][3]};
       if constexpr (AMODE == 2 && !WG)
-        *reinterpret_cast<f32x4*>(As + rm_row * LDK + (rm_kq0 + 2 * u) * 4) = v;
+        *reinterpret_cast<f32x4*>(As + rm_row * LDK + (kw + 2 * u) * 4) = v;
       else
         *reinterpret_cast<f32x4*>(As + (km_row + 32 * u) * LDK + km_kq) = v;
     }
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
       if constexpr (WG)
         *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
       else
-        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + (rm_kq0 + 2 * u) * 4) = v;
+        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + (kw + 2 * u) * 4) = v;
     }
   };
 
@@ -416,14 +430,20 @@ template <bool WG>
 int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   dim3 block(NTHR);
-#define MST_GEMM_CASE(TP)                                                             \
-  case TP:                                                                            \
-    if (WG || p.a_mode == 0)                                                          \
-      hipLaunchKernelGGL((gemm_kernel<TP, WG, 0>), grid, block, 0, st, p);            \
-    else if (p.a_mode == 1)                                                           \
-      hipLaunchKernelGGL((gemm_kernel<TP, WG, (WG ? 0 : 1)>), grid, block, 0, st, p); \
-    else                                                                              \
-      hipLaunchKernelGGL((gemm_kernel<TP, WG, (WG ? 0 : 2)>), grid, block, 0, st, p); \
+#define MST_GEMM_LAUNCH(TP, AM)                                                      \
+  if (p.dual)                                                                        \
+    hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, true>), grid, block, 0, st, p);      \
+  else                                                                               \
+    hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, false>), grid, block, 0, st, p);
+#define MST_GEMM_CASE(TP)                                                            \
+  case TP:                                                                           \
+    if (WG || p.a_mode == 0) {                                                       \
+      MST_GEMM_LAUNCH(TP, 0)                                                         \
+    } else if (p.a_mode == 1) {                                                      \
+      MST_GEMM_LAUNCH(TP, (WG ? 0 : 1))                                              \
+    } else {                                                                         \
+      MST_GEMM_LAUNCH(TP, (WG ? 0 : 2))                                              \
+    }                                                                                \
     break;
   switch (taps) {
     MST_GEMM_CASE(1)
@@ -434,6 +454,7 @@ int launch(const GP& p, hipStream_t st, int taps) {
     default: return MST_EINVAL;
   }
 #undef MST_GEMM_CASE
+#undef MST_GEMM_LAUNCH
   MST_CHECK_LAUNCH();
   if (p.splitk > 1) {
     long long total = (long long)p.M * p.N;
@@ -455,11 +476,23 @@ void fill_src(GP& p, const mst_src* s, int Ctot) {
   p.T0 = s[0].T;
   p.off0 = s[0].off;
   p.x1 = s[1].C > 0 ? s[1].p : nullptr;
+  p.dual = s[1].C > 0;
   p.sb1 = s[1].sb;
   p.sc1 = s[1].sc;
   p.T1 = s[1].T;
   p.off1 = s[1].off;
+  p.C1 = s[1].C;
   if (s[1].C <= 0) p.C0 = Ctot;  // single source covers all channels
+}
+
+// Elements reachable through each source descriptor; every buffer must stay below the 2 GB
+// that the 32-bit buffer offsets (and the OOB sentinel) can address.
+int src_extent(GP& p, int B) {
+  p.nx0 = (long long)(B - 1) * p.sb0 + (long long)(p.C0 - 1) * p.sc0 + p.T0;
+  p.nx1 = p.dual ? (long long)(B - 1) * p.sb1 + (long long)(p.C1 - 1) * p.sc1 + p.T1 : 0;
+  MST_REQUIRE(p.sb0 >= 0 && p.sc0 >= 0 && p.sb1 >= 0 && p.sc1 >= 0);
+  MST_REQUIRE(p.nx0 * 4 < (long long)OOB && p.nx1 * 4 < (long long)OOB);
+  return MST_OK;
 }
 
 int build_conv(const mst_conv_desc* d, GP& p) {
@@ -483,6 +516,10 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   const long long am = d->sAm < 0 ? -d->sAm : d->sAm;
   p.a_mode = kvec ? 1 : (am <= 8 ? 2 : 0);
   fill_src(p, d->src, d->Ctot);
+  p.nA = (long long)(p.M - 1) * d->sAm + (long long)(d->Ctot - 1) * d->sAc +
+         (long long)(d->taps - 1) * d->sAt + 1;
+  MST_REQUIRE(d->sAm >= 0 && d->sAc >= 0 && d->sAt >= 0);
+  MST_REQUIRE(src_extent(p, d->B) == MST_OK && p.nA * 4 < (long long)OOB);
   p.Tv = d->Tv;
   p.ta = d->a;
   p.tb = d->beta;
@@ -529,6 +566,8 @@ int build_wgrad(const mst_wgrad_desc* d, GP& p) {
   p.Tk = d->Tk;
   p.invTk = 1.0f / (float)d->Tk;
   fill_src(p, d->src, d->Ctot);
+  p.nP = (long long)(d->B - 1) * d->sPb + (long long)(d->M - 1) * d->sPc + d->Tk;
+  MST_REQUIRE(src_extent(p, d->B) == MST_OK && p.nP * 4 < (long long)OOB);
   p.Tv = d->Tv;
   p.ta = d->a;
   p.tb = d->beta;
