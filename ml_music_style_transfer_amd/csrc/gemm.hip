@@ -414,16 +414,30 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GP p) {
   }
 }
 
+// Split-K from a wave-quantisation cost model. 256 CUs x 2 resident workgroups = 512 slots;
+// a workgroup's time is ~ (its K tiles) x tau. A trailing partial wave of <= 256 workgroups
+// runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave. Split-K
+// adds a slab round trip (s + 2 passes over M x N floats at ~5 TB/s) plus a launch.
 int choose_splitk(int M, int N, int nk, int req) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
-  long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
-  const long long target = 512;  // two workgroups per CU on 256 CUs
-  if (tiles >= 384 || nk < 16) return 1;
-  int s = (int)((target + tiles - 1) / tiles);
-  int maxs = nk / 8;  // at least eight K tiles per split
-  if (s > maxs) s = maxs;
-  if (s > 32) s = 32;
-  return s < 1 ? 1 : s;
+  const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
+  const double slots = 512.0, tau = 3.4e-6;  // s per 32-deep K tile of one workgroup
+  auto waves = [&](long long n) {
+    long long full = n / (long long)slots, rem = n % (long long)slots;
+    return (double)full + (rem == 0 ? 0.0 : (rem <= slots / 2 ? 0.55 : 1.0));
+  };
+  int best = 1;
+  double best_t = waves(tiles) * nk * tau;
+  const int maxs = nk / 4 < 32 ? nk / 4 : 32;  // at least four K tiles per split
+  for (int s = 2; s <= maxs; ++s) {
+    const double t = waves(tiles * s) * ceil_div(nk, s) * tau +
+                     (double)M * N * 4.0 * (s + 2) / 5e12 + 4e-6;
+    if (t < best_t * 0.97) {
+      best_t = t;
+      best = s;
+    }
+  }
+  return best;
 }
 
 template <bool WG>
