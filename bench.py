@@ -115,6 +115,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-timing-steps", type=int, default=2)
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="all-reduce after backward instead of overlapped bucket all-reduces")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,6 +142,8 @@ def main():
     model = PerformanceNet().to(dev)
     model.train()
     dp.broadcast_parameters(model)
+    if world > 1 and not args.no_overlap:
+        dp.enable_overlapped_allreduce(model)
     opt = make_optimizer(model, lr=1e-3)
 
     # synthetic per-rank data, resident in HBM: target clips, style-reference clips, rolls
@@ -157,9 +161,10 @@ def main():
         split = torch.split(data, 128, dim=1)                      # train.py:130
         y = model(split[0], x_audio, split[1])
         loss = E.l1_loss(y, target)
-        loss.backward()
-        dp.allreduce_gradients(model)
-        opt.step()
+        loss.backward()               # overlapped bucket all-reduces start inside backward
+        if world > 1 and args.no_overlap:
+            dp.allreduce_gradients(model)
+        opt.step()                    # waits for the all-reduce before the update
         return loss
 
     for _ in range(args.warmup):

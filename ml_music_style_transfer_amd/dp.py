@@ -11,6 +11,7 @@ import torch
 import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 256 << 20  # 256 MB: big buckets suit xGMI point-to-point rings
+OVERLAP_BUCKET_BYTES = 128 << 20  # smaller when overlapped: the last bucket is the exposed one
 
 
 def is_dist():
@@ -51,3 +52,104 @@ def allreduce_gradients(model, bucket_bytes=DEFAULT_BUCKET_BYTES, async_op=False
 def wait_all(works):
     for w in works:
         w.wait()
+
+
+class OverlappedAllReduce:
+    """Gradient all-reduce overlapped with the backward pass.
+
+    The model's flat gradient buffer is laid out in the order backward produces gradients
+    (engine.backward_param_order), so it is cut into contiguous buckets at parameter
+    boundaries that complete front to back. The backward program reports finished blocks
+    (GradSink.block_done -> ready); as soon as every parameter of the next bucket is done, its
+    all-reduce is issued from the compute stream (RCCL's stream waits for the gradient
+    kernels already enqueued, later backward kernels keep running beside it). Buckets are
+    issued strictly in order, so every rank issues the same collectives in the same order.
+    `finish()` (called by Adam.step or dp.finish_gradients) makes the compute stream wait.
+
+    Gradient accumulation stays correct: the part of a bucket accumulated in earlier
+    backward passes is identical on all ranks, so averaging the sum averages the new part.
+    """
+
+    def __init__(self, model, bucket_bytes=OVERLAP_BUCKET_BYTES):
+        self.model = model
+        _, grad, n = model.flat_buffers()
+        f = model._flat
+        params = model._flat_params_list()
+        spans = sorted((f["index"][id(p)][0], f["index"][id(p)][1], id(p)) for p in params)
+        per = max(1, bucket_bytes // 4)
+        self.buckets = []     # [start, end) element ranges of the flat gradient buffer
+        self.bucket_of = {}   # id(param) -> bucket index
+        self.count = []       # parameters per bucket
+        start = 0
+        members = []
+        for i, (o, k, pid) in enumerate(spans):
+            members.append(pid)
+            last = i == len(spans) - 1
+            end = n if last else spans[i + 1][0]
+            if end - start >= per or last:
+                b = len(self.buckets)
+                self.buckets.append((start, end))
+                self.count.append(len(members))
+                for q in members:
+                    self.bucket_of[q] = b
+                members = []
+                start = end
+        self.grad = grad
+        self.works = []
+        self.remaining = list(self.count)
+        self.next = 0
+        self.active = False
+
+    def begin(self):
+        self.remaining = list(self.count)
+        self.next = 0
+        self.works = []
+        self.active = is_dist()
+
+    def _launch(self, b):
+        s, e = self.buckets[b]
+        op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
+        self.works.append(dist.all_reduce(self.grad[s:e], op=op, async_op=True))
+
+    def ready(self, params):
+        if not self.active:
+            return
+        for p in params:
+            b = self.bucket_of.get(id(p))
+            if b is not None:
+                self.remaining[b] -= 1
+        while self.next < len(self.buckets) and self.remaining[self.next] <= 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def launch_remaining(self):
+        if not self.active:
+            return
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+
+    def finish(self):
+        if not self.active:
+            return
+        self.launch_remaining()
+        for w in self.works:
+            w.wait()
+        if dist.get_backend() != "nccl":
+            self.grad.mul_(1.0 / dist.get_world_size())
+        self.works = []
+        self.active = False
+
+
+def enable_overlapped_allreduce(model, bucket_bytes=OVERLAP_BUCKET_BYTES):
+    """Attach an OverlappedAllReduce to `model`: every backward then all-reduces (averages)
+    the gradients while it runs. The package's Adam waits for it; with another optimizer call
+    finish_gradients(model) between loss.backward() and optimizer.step()."""
+    model._mst_dp = OverlappedAllReduce(model, bucket_bytes)
+    return model._mst_dp
+
+
+def finish_gradients(model):
+    r = getattr(model, "_mst_dp", None)
+    if r is not None:
+        r.finish()

@@ -37,12 +37,19 @@ def _e(shape, like):
 
 
 class GradSink:
-    """Where weight gradients go: p.grad if present (accumulate) else a fresh buffer."""
+    """Where weight gradients go: p.grad if present (accumulate) else a fresh buffer.
 
-    def __init__(self, flat_grad_of=None):
+    `on_ready(params)` (optional) is told, at each block boundary of the backward program,
+    which parameters' gradient kernels have all been launched on the current stream; the
+    data-parallel reducer (dp.OverlappedAllReduce) starts bucket all-reduces from it."""
+
+    def __init__(self, flat_grad_of=None, on_ready=None):
         self.flat_grad_of = flat_grad_of or (lambda p: None)
+        self.on_ready = on_ready
+        self._pending = []
 
     def target(self, p):
+        self._pending.append(p)
         if p.grad is None:
             g = self.flat_grad_of(p)
             if g is None:
@@ -50,6 +57,11 @@ class GradSink:
             p.grad = g
             return g, False
         return p.grad, True
+
+    def block_done(self):
+        if self.on_ready is not None and self._pending:
+            self.on_ready(self._pending)
+        self._pending = []
 
 
 # ------------------------------------------------------------------ DownConv
@@ -259,6 +271,23 @@ def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5):
     return y, state
 
 
+def backward_param_order(depth=5):
+    """Parameter names in the order network_bwd produces their gradients (the flat buffer's
+    layout, so data-parallel buckets complete front to back during the backward pass)."""
+    names = ["lastconv.weight", "lastconv.bias"]
+    blk = lambda prefix, group: [f"{prefix}.{n}" for n in group]  # noqa: E731
+    for i in reversed(range(depth - 1)):
+        names += blk(f"up_convs.{i}", UP[4:] + UP[2:4] + UP[:2])
+        names += blk(f"dense_concats.{i + 1}", DN[2:] + DN[:2])
+    names += blk("dense_concats.0", DN[2:] + DN[:2])
+    for i in (2, 1, 0):
+        names += blk(f"onset_offset_encoder.down_convs.{i}", DC[2:] + DC[:2])
+    for name in ("down_convs", "down_convs_audio"):
+        for i in reversed(range(depth)):
+            names += blk(f"{name}.{i}", DC[2:] + DC[:2])
+    return names
+
+
 def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
     depth = st["depth"]
     y = st["y"]
@@ -269,6 +298,7 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
     K.convT1_wgrad(x_dec, dypre, g, acc, scale=MBR_SCALE)
     g, acc = sink.target(P["lastconv.bias"])
     K.bias_grad(dypre, g, acc)
+    sink.block_done()
     dx = torch.empty_like(x_dec)
     K.convT1_dgrad(dypre, W, dx, alpha=MBR_SCALE)
     del dypre
@@ -283,23 +313,29 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
         d_res_pre, dx, d_cd = upconv_bwd(_pp(P, f"up_convs.{i}", UP), st["sv_up"][i], sink, dx,
                                          res_gate=svd[3], res_gate_scale=s, dec_gate=dec_gate,
                                          dec_gate_scale=1.0 / (1.0 - sv_d0[4]))
+        sink.block_done()
         if i < 2:
             d_conds[(i - 1) % 2] = d_cd
         d_midi, d_audio = dense_bwd(_pp(P, f"dense_concats.{i + 1}", DN), svd, sink, d_res_pre,
                                     gated=True)
+        sink.block_done()
         d_before_m[depth - 2 - i] = d_midi
         d_before_a[depth - 2 - i] = d_audio
     d_xm, d_xa = dense_bwd(_pp(P, "dense_concats.0", DN), sv_d0, sink, dx, gated=True)
+    sink.block_done()
     del dx
     # onset/offset encoder: level 2 pooled = conds[1], level 1 pooled = conds[0] and level-2 input
     sv_o = st["sv_o"]
     d2 = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.2", DC), sv_o[2], sink,
                       d_pool0=d_conds[1])
+    sink.block_done()
     d1 = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.1", DC), sv_o[1], sink,
                       d_pool0=d_conds[0], d_pool1=d2)
+    sink.block_done()
     del d2
     d_cond_in = downconv_bwd(_pp(P, "onset_offset_encoder.down_convs.0", DC), sv_o[0], sink,
                              d_pool0=d1, need_dx=need_input_grads[2])
+    sink.block_done()
     del d1
     grads_in = []
     for name, sv, d_before, d_top in (("down_convs", st["sv_m"], d_before_m, d_xm),
@@ -309,10 +345,12 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
             prm = _pp(P, f"{name}.{i}", DC)
             if i == depth - 1:  # no pooling: before_pool is the output
                 d_pool = downconv_bwd(prm, sv[i], sink, d_before=d_top, need_dx=True)
+                sink.block_done()
             else:
                 need = i > 0 or need_input_grads[0 if name == "down_convs" else 1]
                 d_pool = downconv_bwd(prm, sv[i], sink, d_before=d_before[i], d_pool0=d_pool,
                                       need_dx=need)
+            sink.block_done()
             d_before[i] = None
         grads_in.append(d_pool)
     return grads_in[0], grads_in[1], d_cond_in
@@ -338,7 +376,13 @@ class PerformanceNetFunction(torch.autograd.Function):
         module = ctx.module
         P = module._param_dict()
         need = (ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.needs_input_grad[3])
-        g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), module._grad_sink(), need)
+        reducer = getattr(module, "_mst_dp", None)  # dp.OverlappedAllReduce, if attached
+        if reducer is not None:
+            reducer.begin()
+        sink = module._grad_sink(reducer.ready if reducer is not None else None)
+        g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need)
+        if reducer is not None:
+            reducer.launch_remaining()
         ctx.state = None
         n_params = len(module._flat_params_list())
         return (None, g_m if need[0] else None, g_a if need[1] else None,

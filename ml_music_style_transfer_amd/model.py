@@ -338,14 +338,19 @@ class PerformanceNet(nn.Module):
 
     def flatten_parameters_(self):
         """Move trainable parameters into one contiguous device buffer (16-B aligned slots)."""
-        params = self._flat_params_list()
+        named = self._trainable_named()
+        params = [p for _, p in named]
         dev = params[0].device
-        offsets, off = [], 0
-        for p in params:
-            offsets.append(off)
-            off += (p.numel() + 3) // 4 * 4
-        flat = torch.empty(off, device=dev, dtype=torch.float32)
-        grad = torch.empty(off, device=dev, dtype=torch.float32)
+        # Slots are laid out in the order backward produces the gradients (lastconv first,
+        # the input-side encoder levels last) so data-parallel buckets fill front to back.
+        rank = {n: i for i, n in enumerate(E.backward_param_order(self.depth))}
+        order = sorted(range(len(named)), key=lambda i: (rank.get(named[i][0], len(rank)), i))
+        offsets, off = [0] * len(params), 0
+        for i in order:
+            offsets[i] = off
+            off += (params[i].numel() + 3) // 4 * 4
+        flat = torch.zeros(off, device=dev, dtype=torch.float32)
+        grad = torch.zeros(off, device=dev, dtype=torch.float32)
         with torch.no_grad():
             for p, o in zip(params, offsets):
                 flat[o:o + p.numel()].copy_(p.data.reshape(-1))
@@ -368,7 +373,7 @@ class PerformanceNet(nn.Module):
         f = self._flat
         return f["param"], f["grad"], f["numel"]
 
-    def _grad_sink(self):
+    def _grad_sink(self, on_ready=None):
         f = self._flat
 
         def flat_grad_of(p):
@@ -377,7 +382,7 @@ class PerformanceNet(nn.Module):
                 return None
             o, n = ent
             return f["grad"][o:o + n].view_as(p)
-        return E.GradSink(flat_grad_of)
+        return E.GradSink(flat_grad_of, on_ready)
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)

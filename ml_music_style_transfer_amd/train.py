@@ -20,6 +20,7 @@ import os
 import numpy as np
 import torch
 
+from . import dp
 from . import engine as E
 from . import kernels as K
 from .model import PerformanceNet
@@ -87,6 +88,10 @@ class Adam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        owner = getattr(self, "_owner", None)
+        reducer = getattr(owner, "_mst_dp", None) if owner is not None else None
+        if reducer is not None:
+            reducer.finish()  # overlapped data-parallel all-reduce must land first
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             lr, eps = group["lr"], group["eps"]
@@ -152,6 +157,7 @@ def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2):
         y_pred = model(_cuda(split[0]), _cuda(data_cond), _cuda(split[1]))
         loss = E.l1_loss(y_pred, _cuda(target))
         loss.backward()
+        dp.finish_gradients(model)  # no-op unless an overlapped DP all-reduce is attached
         iter_train_loss.append(loss.item())
         train_loss += loss
         optimizer.step()

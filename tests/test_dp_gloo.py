@@ -82,3 +82,69 @@ def test_per_rank_mean_gradients_average_to_full_batch():
     full = grad(x, t)
     halves = (grad(x[:2], t[:2]) + grad(x[2:], t[2:])) / 2
     torch.testing.assert_close(halves, full)
+
+
+class _LayeredModel:
+    """Stand-in exposing what OverlappedAllReduce uses of PerformanceNet's flat buffers."""
+
+    def __init__(self, sizes, rank):
+        self.params = [torch.nn.Parameter(torch.empty(k)) for k in sizes]
+        offs, off = [], 0
+        for k in sizes:
+            offs.append(off)
+            off += (k + 3) // 4 * 4
+        self.flat = torch.zeros(off)
+        self.gradbuf = torch.zeros(off)
+        g = torch.Generator().manual_seed(7 + rank)
+        for p, o in zip(self.params, offs):
+            self.gradbuf[o:o + p.numel()] = torch.randn(p.numel(), generator=g)
+        self._flat = {"index": {id(p): (o, p.numel()) for p, o in zip(self.params, offs)}}
+        self.n = off
+
+    def flat_buffers(self):
+        return self.flat, self.gradbuf, self.n
+
+    def _flat_params_list(self):
+        return self.params
+
+
+def _overlap_worker(rank, world, port, sizes, bucket, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ml_music_style_transfer_amd import dp
+    m = _LayeredModel(sizes, rank)
+    r = dp.OverlappedAllReduce(m, bucket_bytes=bucket)
+    r.begin()
+    launched = []
+    for i in range(0, len(m.params), 2):   # "blocks" of two parameters finish in layout order
+        r.ready(m.params[i:i + 2])
+        launched.append(r.next)
+    r.finish()
+    q.put((rank, m.gradbuf.clone(), len(r.buckets), launched))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_bucket_allreduce_gloo():
+    """Buckets are issued as soon as their parameters are done, in order, and the result is
+    the rank average (dp.OverlappedAllReduce, the path bench.py uses for N > 1)."""
+    sizes = [5, 17, 3, 64, 9, 1, 33, 8]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, sizes, 4 * 24, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, nb, la)) for r, g, nb, la in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mean = sum(_LayeredModel(sizes, r).gradbuf for r in range(world)) / world
+    for r in range(world):
+        g, nb, launched = res[r]
+        assert nb > 2
+        assert launched == sorted(launched) and launched[0] >= 1  # issued during "backward"
+        torch.testing.assert_close(g, mean, rtol=1e-6, atol=1e-6)
