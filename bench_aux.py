@@ -1,0 +1,234 @@
+"""Secondary measurements (not the driver's bench line): BASELINE.json configs[1] and [4].
+
+  frontend    config 2: batched STFT log-power and 128-mel of 256 x 4 s @ 16 kHz clips
+              (preprocess.py:47-49, tests/plot_spec.py:20). HBM roofline: algorithmic bytes per
+              clip 4 L + 4 F T (log-power) and 4 L + 4 M T (mel).
+  griffinlim  config 2: 60-iteration Griffin-Lim of the same 256 spectrograms (inference.py:105-110).
+              Algorithmic bytes per iteration per clip 28 F T + 8 L.
+  mss         config 5: multi-scale spectral loss (6 FFT sizes) forward + gradient on
+              10 s @ 22.05 kHz clip pairs (pred = target + 0.05 N(0,1), seed 7). Algorithmic
+              bytes per clip pair 6 x 5 x 4 L (SURVEY 8(d)'s per-size streaming model; the fused
+              kernel moves 12 B per sample once, so `frac` may exceed 1).
+
+Each workload prints one JSON line with the same fields as bench.py (value = whole-job
+throughput with inputs resident in HBM; kernel time by HIP events on the launch stream) and
+a cpu_baseline from the oracle on a bounded sample. N > 1 under torch.distributed.run shards
+clips across ranks (independent units, no collective).
+
+usage: python bench_aux.py [--workload frontend|griffinlim|mss|all] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402  (synthetic clip recipe)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
+
+
+def _dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    return world, rank, dev
+
+
+def _timed(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device="cuda")
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        dt = tt.item()
+    return dt / steps
+
+
+def _event_ms(fn, reps=5):
+    """Average duration of fn's launches, HIP events on the current (launch) stream."""
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def _roof(achieved_gbs, kernel, bytes_per_launch):
+    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved_gbs, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+            "traffic": None, "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+
+
+def _line(metric, value, unit, world, steps, warmup, ms, config, roofline, cpu, extra=None):
+    out = {"metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world,
+           "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+           "config": config, "roofline": roofline}
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    if extra:
+        out.update(extra)
+    return out
+
+
+def frontend(args, world, rank, dev):
+    from ml_music_style_transfer_amd import spectral
+    from oracle import spectral_ref as SR
+    B, L, F, M = args.clips, bench.L_SAMPLES, 1025, 128
+    T = 1 + L // bench.HOP
+    x, _ = bench.synth_clips(B, 4242 + 100_000 * rank)
+    xd = torch.from_numpy(x).to(dev)
+    res = []
+    for name, fn, bpc, kern in (
+            ("logpow", lambda: spectral.stft_logpow(xd, hop=bench.HOP), 4 * L + 4 * F * T,
+             "stft_kernel<LOGPOW>"),
+            ("mel", lambda: spectral.melspectrogram(xd, bench.SR, hop_length=bench.HOP), 4 * L + 4 * M * T,
+             "stft_kernel<MEL>")):
+        dt = _timed(fn, args.steps, args.warmup, world)
+        kms = _event_ms(fn)
+        cpu = None
+        if rank == 0 and not args.no_cpu_baseline:
+            n = 16
+            t0 = time.perf_counter()
+            for i in range(n):
+                (SR.logpow(x[i], 2048, bench.HOP) if name == "logpow"
+                 else SR.melspec(x[i], bench.SR, 2048, bench.HOP))
+            c = (time.perf_counter() - t0) / n
+            cpu = {"value": round(1.0 / c, 2), "unit": "clips/s", "cores": 1, "kind": "port",
+                   "sample": f"{n} clips through oracle/spectral_ref.py (NumPy pocketfft float64, 1 thread)"}
+        res.append(_line(f"STFT {name} clips/s, 256 x 4 s @ 16 kHz", world * B / dt, "clips/s", world,
+                         args.steps, args.warmup, dt * 1e3,
+                         {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,
+                          "n_fft": 2048, "hop": bench.HOP},
+                         _roof(B * bpc / (kms * 1e-3) / 1e9, kern, B * bpc), cpu,
+                         {"kernel_ms": round(kms, 4)}))
+    return res
+
+
+def griffinlim(args, world, rank, dev):
+    from ml_music_style_transfer_amd import spectral
+    from oracle import spectral_ref as SR
+    B, L, F = args.clips, bench.L_SAMPLES, 1025
+    T = 1 + L // bench.HOP
+    x, _ = bench.synth_clips(B, 5151 + 100_000 * rank)
+    S = spectral.stft_power(torch.from_numpy(x).to(dev), hop=bench.HOP).clamp_min(0).sqrt()
+    n_iter = 60
+
+    def fn():
+        return spectral.griffinlim(S, n_iter=n_iter, hop_length=bench.HOP, init=None)
+
+    steps = max(1, args.steps // 4)
+    dt = _timed(fn, steps, 1, world)
+    kms = _event_ms(fn, reps=2)
+    bpi = 28 * F * T + 8 * L
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        Sn = np.abs(SR.stft(x[0], 2048, bench.HOP, out_dtype=None))
+        t0 = time.perf_counter()
+        SR.griffinlim(Sn, n_iter=10, hop=bench.HOP, angles=np.ones_like(Sn, dtype=np.complex128))
+        c = (time.perf_counter() - t0) / 10
+        cpu = {"value": round(1.0 / (c * n_iter), 3), "unit": "clips/s (60 iterations)", "cores": 1,
+               "kind": "port", "sample": "1 clip x 10 iterations of oracle/spectral_ref.griffinlim "
+                                         "(NumPy float64, 1 thread), scaled to 60 iterations"}
+    return [_line("Griffin-Lim clips/s (60 iterations), 256 x 4 s @ 16 kHz", world * B / dt,
+                  "clips/s", world, steps, 1, dt * 1e3,
+                  {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
+                   "L": L, "n_fft": 2048, "hop": bench.HOP},
+                  _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9, "istft_kernel + stft_kernel<COMPLEX> per iteration",
+                        B * n_iter * bpi), cpu, {"kernel_ms": round(kms, 3)})]
+
+
+def mss(args, world, rank, dev):
+    from ml_music_style_transfer_amd import spectral
+    from oracle import spectral_ref as SR
+    B, L = args.pairs, 220_500
+    sizes = spectral.MSS_SIZES
+    rng = np.random.default_rng(7 + 1000 * rank)
+    x, _ = bench.synth_clips(B, 9090 + 100_000 * rank, L=L, sr=22050)
+    tgt = torch.from_numpy(x).to(dev)
+    pred = (tgt + 0.05 * torch.from_numpy(rng.standard_normal((B, L)).astype(np.float32)).to(dev))
+    pred.requires_grad_(True)
+
+    def fn():
+        pred.grad = None
+        loss = spectral.multiscale_spectral_loss(pred, tgt, sizes=sizes)
+        loss.backward()
+        return loss
+
+    dt = _timed(fn, args.steps, args.warmup, world)
+    kms = _event_ms(fn)
+    bpp = len(sizes) * 5 * 4 * L
+    flops = sum(3 * 4 * 2.5 * n * np.log2(n) * (1 + L // (n // 4)) / 4 for n in sizes)  # rough
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        p64 = pred.detach()[0].cpu().double().numpy()
+        t64 = tgt[0].cpu().double().numpy()
+        t0 = time.perf_counter()
+        SR.multiscale_spectral_loss_grad(p64, t64, 1.0, 1e-7, sizes)
+        c = time.perf_counter() - t0
+        cpu = {"value": round(1.0 / c, 3), "unit": "clip-pairs/s", "cores": 1, "kind": "port",
+               "sample": "1 clip pair (10 s @ 22.05 kHz), loss + gradient by "
+                         "oracle/spectral_ref.multiscale_spectral_loss_grad (NumPy float64)"}
+    return [_line("multi-scale spectral loss fwd+grad clip-pairs/s, 10 s @ 22.05 kHz, 6 FFT sizes",
+                  world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
+                  {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
+                   "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
+                  _roof(B * bpp / (kms * 1e-3) / 1e9, "mss_scale_kernel<6..11> + fold + loss reduce",
+                        B * bpp), cpu,
+                  {"kernel_ms": round(kms, 4), "approx_fft_gflop_per_step": round(B * flops / 1e9, 2)})]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="all", choices=["frontend", "griffinlim", "mss", "all"])
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=256)
+    ap.add_argument("--pairs", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    world, rank, dev = _dist()
+    from ml_music_style_transfer_amd import _lib
+    _lib.load()
+    lines = []
+    for wl, fn in (("frontend", frontend), ("griffinlim", griffinlim), ("mss", mss)):
+        if args.workload in (wl, "all"):
+            lines += fn(args, world, rank, dev)
+    if rank == 0:
+        for ln in lines:
+            print(json.dumps(ln), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

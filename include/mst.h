@@ -198,6 +198,16 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
                        float momentum, const float* angles0, int32_t mag_from_logpow, float* y,
                        void* workspace, size_t ws_bytes, void* stream);
 
+/* ---- multi-scale spectral loss (DDSP; README.md:23, stub train.py:119-123; build-defined) ----
+ * pred, target (B, L) waveforms; sizes[n_sizes] FFT sizes, powers of two in [64, 2048], hop n/4,
+ * periodic Hann, center + reflect pad (L > n/2). loss (1 device float) =
+ *   sum_n mean|S_n(pred) - S_n(target)| + alpha mean|log(S_n(pred)+eps) - log(S_n(target)+eps)|
+ * dpred (B, L) (nullable) receives d loss / d pred. sizes is a HOST array (<= 8 entries). */
+size_t mst_mss_workspace_size(int64_t B, int64_t L, int32_t n_sizes, const int32_t* sizes);
+int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t L, int32_t n_sizes,
+                     const int32_t* sizes, float alpha, float eps, float* loss, float* dpred,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 /* ---- piano roll (preprocess.py:148-155): roll (B, T, 128) velocities ->
  *      binarised roll and onoff, both (B, T, 128) ---- */
 int mst_onoff_f32(const float* roll, int32_t B, int32_t T, float* bin, float* onoff, void* stream);

@@ -91,6 +91,10 @@ SIGNATURES = {
     "mst_griffinlim_workspace_size": (c_size_t, [c_int32, c_int32, c_int32, c_int32]),
     "mst_griffinlim_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_float,
                                      c_void_p, c_int32, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mst_mss_workspace_size": (c_size_t, [ctypes.c_int64, ctypes.c_int64, c_int32, c_void_p]),
+    "mst_mss_loss_f32": (c_int32, [c_void_p, c_void_p, ctypes.c_int64, ctypes.c_int64, c_int32,
+                                   c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p,
+                                   c_size_t, c_void_p]),
     "mst_onoff_f32": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "mst_version": (ctypes.c_char_p, []),
     "mst_device_arch": (c_int32, [ctypes.c_char_p, c_int32]),

@@ -111,3 +111,72 @@ def test_griffinlim_vs_oracle(cuda):
     logp = np.log1p(S.astype(np.float64) ** 2).astype(np.float32)
     audio = AudioSynthesizer.griffinlim(None, logp, 1, n_iter=5)
     assert audio.shape == (256 * (T - 1),) and np.isfinite(audio).all()
+
+
+def _mss_pair(B, L, seed):
+    rng = np.random.default_rng(seed)
+    t = np.arange(L) / 22050.0
+    f0 = rng.uniform(100, 1000, size=(B, 1))
+    tgt = (0.4 * np.sin(2 * np.pi * f0 * t) * np.exp(-2 * t) + 0.05 * rng.standard_normal((B, L)))
+    pred = tgt + 0.05 * rng.standard_normal((B, L))   # target + 0.05 N(0,1)
+    return pred.astype(np.float32), tgt.astype(np.float32)
+
+
+@pytest.mark.parametrize("B,L,sizes", [(2, 5003, (2048, 1024, 512, 256, 128, 64)),
+                                       (3, 1500, (1024, 128)),
+                                       (1, 700, (64,)),
+                                       (2, 220_500, (2048, 1024, 512, 256, 128, 64))])
+def test_multiscale_spectral_loss_and_grad(cuda, B, L, sizes):
+    """mss.hip vs the float64 oracle (parity unpinned: the reference only has the idea, README.md:23).
+    Loss within 1e-4 relative (north_star's fp32 bound on loss values). The gradient is judged
+    like the model's: G = sign(dS)(1 + alpha/(S+eps)) amplifies fp32 rounding of the smallest
+    bins, so torch's own fp32 path (torch.stft autograd on the CPU) is 0.6-3% (relative L2) off
+    the float64 gradient here; ours must be within max(that gap, 1e-3).
+    The last case is config 5's clip length (10 s @ 22.05 kHz)."""
+    from ml_music_style_transfer_amd import spectral
+    p, q = _mss_pair(B, L, 11)
+    loss64, d64 = SR.multiscale_spectral_loss_grad(p.astype(np.float64), q.astype(np.float64),
+                                                   1.0, 1e-7, sizes)
+    pt = torch.from_numpy(p).to(cuda).requires_grad_(True)
+    qt = torch.from_numpy(q).to(cuda)
+    loss = spectral.multiscale_spectral_loss(pt, qt, sizes=sizes)
+    (2.0 * loss).backward()
+    assert abs(loss.item() - loss64) <= 1e-4 * abs(loss64)
+    d = pt.grad.cpu().numpy().astype(np.float64) / 2.0
+    rel = np.linalg.norm(d - d64) / np.linalg.norm(d64)
+    assert rel <= max(_torch_fp32_mss_grad_gap(p, q, sizes, d64), 1e-3), rel
+
+
+def _torch_fp32_mss_grad_gap(p, q, sizes, d64):
+    pt = torch.tensor(p, requires_grad=True)
+    qt = torch.tensor(q)
+    tot = 0
+    for n in sizes:
+        w = torch.hann_window(n, periodic=True)
+        a = torch.stft(pt, n, n // 4, window=w, center=True, pad_mode="reflect",
+                       return_complex=True).abs()
+        b = torch.stft(qt, n, n // 4, window=w, center=True, pad_mode="reflect",
+                       return_complex=True).abs()
+        tot = tot + (a - b).abs().mean() + (torch.log(a + 1e-7) - torch.log(b + 1e-7)).abs().mean()
+    tot.backward()
+    return np.linalg.norm(pt.grad.numpy().astype(np.float64) - d64) / np.linalg.norm(d64)
+
+
+def test_multiscale_spectral_loss_identical_inputs(cuda):
+    from ml_music_style_transfer_amd import spectral
+    p, _ = _mss_pair(2, 30_000, 5)
+    pt = torch.from_numpy(p).to(cuda).requires_grad_(True)
+    loss = spectral.multiscale_spectral_loss(pt, pt.detach().clone())
+    loss.backward()
+    # p and q are packed in one complex transform, so |P| and |Q| agree to rounding, not bits
+    assert 0.0 <= loss.item() < 1e-5
+    assert torch.isfinite(pt.grad).all()
+
+
+def test_multiscale_spectral_loss_rejects_bad_sizes(cuda):
+    from ml_music_style_transfer_amd import spectral
+    x = torch.zeros(1, 1000, device=cuda)
+    with pytest.raises(ValueError):
+        spectral.multiscale_spectral_loss(x, x, sizes=(48,))
+    with pytest.raises(ValueError):
+        spectral.multiscale_spectral_loss(x, x, sizes=(2048,))   # needs L > n/2
