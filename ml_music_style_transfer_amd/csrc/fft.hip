@@ -79,6 +79,37 @@ __device__ __forceinline__ void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
   }
 }
 
+// exp(-2 pi i j / 32), j = 0..15 (forward sign), folded to immediates.
+constexpr float kW32C[16] = {1.000000000f, 0.980785280f, 0.923879533f, 0.831469612f, 0.707106781f,
+                             0.555570233f, 0.382683432f, 0.195090322f, 0.000000000f, -0.195090322f,
+                             -0.382683432f, -0.555570233f, -0.707106781f, -0.831469612f,
+                             -0.923879533f, -0.980785280f};
+constexpr float kW32S[16] = {0.000000000f, -0.195090322f, -0.382683432f, -0.555570233f,
+                             -0.707106781f, -0.831469612f, -0.923879533f, -0.980785280f,
+                             -1.000000000f, -0.980785280f, -0.923879533f, -0.831469612f,
+                             -0.707106781f, -0.555570233f, -0.382683432f, -0.195090322f};
+// v[k] *= w^k for k = 1..15, powers by a depth-4 product tree (one table lookup per pass
+// instead of fifteen; error a few ulp).
+__device__ __forceinline__ void twiddle_powers(c2 v[16], c2 w1) {
+  const c2 w2 = cmul(w1, w1), w4 = cmul(w2, w2), w8 = cmul(w4, w4);
+  const c2 w3 = cmul(w2, w1), w5 = cmul(w4, w1), w6 = cmul(w4, w2), w7 = cmul(w4, w3);
+  v[1] = cmul(v[1], w1);
+  v[2] = cmul(v[2], w2);
+  v[3] = cmul(v[3], w3);
+  v[4] = cmul(v[4], w4);
+  v[5] = cmul(v[5], w5);
+  v[6] = cmul(v[6], w6);
+  v[7] = cmul(v[7], w7);
+  v[8] = cmul(v[8], w8);
+  v[9] = cmul(v[9], cmul(w8, w1));
+  v[10] = cmul(v[10], cmul(w8, w2));
+  v[11] = cmul(v[11], cmul(w8, w3));
+  v[12] = cmul(v[12], cmul(w8, w4));
+  v[13] = cmul(v[13], cmul(w8, w5));
+  v[14] = cmul(v[14], cmul(w8, w6));
+  v[15] = cmul(v[15], cmul(w8, w7));
+}
+
 // W16^m as compile-time constants (forward sign).
 __device__ __forceinline__ c2 w16(int m) {
   constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654752f;
@@ -130,8 +161,7 @@ template <bool INV>
 __device__ void fft1024(c2 v[16], c2* S, const c2* qt, int lane) {
   // pass A: radix-16 over j, twiddle W1024^{lane k1} = W2048^{2 lane k1}
   dft16<INV>(v);
-#pragma unroll
-  for (int k1 = 1; k1 < 16; ++k1) v[k1] = cmul(v[k1], tw<INV>(qt, 2 * lane * k1));
+  twiddle_powers(v, tw<INV>(qt, 2 * lane));  // W1024^{lane k1}
 #pragma unroll
   for (int k1 = 0; k1 < 16; ++k1) S[k1 * RS + lane] = v[k1];
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -142,8 +172,7 @@ __device__ void fft1024(c2 v[16], c2* S, const c2* qt, int lane) {
 #pragma unroll
     for (int jp = 0; jp < 16; ++jp) v[jp] = S[k1 * RS + lp + 4 * jp];
     dft16<INV>(v);
-#pragma unroll
-    for (int mp = 1; mp < 16; ++mp) v[mp] = cmul(v[mp], tw<INV>(qt, 32 * lp * mp));
+    twiddle_powers(v, tw<INV>(qt, 32 * lp));  // W64^{lp mp}
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -180,50 +209,26 @@ __device__ __forceinline__ float hann_w(const c2* qt, int n) {
   return 0.5f - 0.5f * tw<false>(qt, n).x;
 }
 
-// Frame f of clip xr (length L): lanes load the windowed packed input z[lane + 64 j].
-__device__ __forceinline__ void load_frame(const float* xr, int L, int f, int hop, int pad_mode,
-                                           const c2* qt, int lane, c2 v[16]) {
-  const int s0 = f * hop - NFFT / 2;
-  const bool interior = s0 >= 0 && s0 + NFFT <= L && ((((uintptr_t)(xr + s0)) & 7) == 0);
-  if (interior) {
-    const float2* p = reinterpret_cast<const float2*>(xr + s0);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      int n = lane + 64 * j;
-      float2 e = p[n];
-      v[j] = mk(e.x * hann_w(qt, 2 * n), e.y * hann_w(qt, 2 * n + 1));
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      int n = lane + 64 * j;
-      float e[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        int s = s0 + 2 * n + h;
-        float val;
-        if (s >= 0 && s < L) val = xr[s];
-        else if (pad_mode == MST_PAD_CONSTANT) val = 0.f;
-        else {
-          if (s < 0) s = -s;
-          if (s >= L) s = 2 * (L - 1) - s;
-          val = (s >= 0 && s < L) ? xr[s] : 0.f;
-        }
-        e[h] = val * hann_w(qt, 2 * n + h);
-      }
-      v[j] = mk(e[0], e[1]);
-    }
-  }
-}
-
 // Real-FFT post-twist: X[k] for k = lane + 64 j from Z in S; X[1024] via lane 0.
-__device__ __forceinline__ c2 post_bin(const c2* S, const c2* qt, int k) {
+__device__ __forceinline__ c2 post_bin(const c2* S, c2 wk, int k) {
   c2 A = S[k];
   c2 Bc = conj(S[(NC - k) & (NC - 1)]);
   c2 xe = (A + Bc) * 0.5f;
   c2 d = A - Bc;
   c2 xo = mk(0.5f * d.y, -0.5f * d.x);  // -i/2 * d
-  return xe + cmul(tw<false>(qt, k), xo);
+  return xe + cmul(wk, xo);
+}
+
+// W2048^(lane + 64 j) from e = W2048^lane.
+__device__ __forceinline__ c2 tw_bin(c2 e, int j) { return cmul(e, mk(kW32C[j], kW32S[j])); }
+
+// Periodic Hann 0.5 - 0.5 cos(2 pi m / 2048) = sin^2(pi m / 2048), in the sin^2 form so the
+// small values at the frame edges keep their relative precision. For m = 2n, n = lane + 64 j:
+// sin(pi m / 2048) = -Im(W2048^n) with W2048^n = e1 W32^j; for m = 2n + 1 the same with
+// eh = W4096^{2 lane + 1}.
+__device__ __forceinline__ float hann_sq(c2 e, int j) {
+  const float s = e.x * kW32S[j] + e.y * kW32C[j];  // Im(e W32^j)
+  return s * s;
 }
 
 __device__ __forceinline__ float log1p_fast(float p) {
@@ -244,145 +249,143 @@ struct MelTab {
   int n_mels;
 };
 
+// Raw (unwindowed) samples of frame f for z[lane + 64 j] (center padding: reflect or zeros).
+__device__ __forceinline__ void fetch_frame(const float* xr, int L, int f, int hop, int pad_mode,
+                                            int lane, float2 raw[16]) {
+  const int s0 = f * hop - NFFT / 2;
+  const bool interior = s0 >= 0 && s0 + NFFT <= L && ((((uintptr_t)(xr + s0)) & 7) == 0);
+  if (interior) {
+    const float2* p = reinterpret_cast<const float2*>(xr + s0);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) raw[j] = p[lane + 64 * j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = lane + 64 * j;
+      float e[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        int s = s0 + 2 * n + h;
+        float val;
+        if (s >= 0 && s < L) val = xr[s];
+        else if (pad_mode == MST_PAD_CONSTANT) val = 0.f;
+        else {
+          if (s < 0) s = -s;
+          if (s >= L) s = 2 * (L - 1) - s;
+          val = (s >= 0 && s < L) ? xr[s] : 0.f;
+        }
+        e[h] = val;
+      }
+      raw[j] = make_float2(e[0], e[1]);
+    }
+  }
+}
+
+// STFT: 512 threads = 8 waves, 32 frames per workgroup in 4 rounds of 8 (one frame per wave).
+// Twiddles and window values come from one per-lane table lookup times compile-time roots of
+// unity (see twiddle_powers / tw_bin / hann_ej); each wave leaves its frame's 1025 results in its own LDS scratch (offset by
+// 8 floats per wave so the transposed read is bank-conflict-free), and after a barrier the
+// workgroup writes the round as (bin, 8 frames) runs of the frequency-major (B, F, T) output.
+// 73.7 KB LDS per workgroup.
 template <int MODE>
-__global__ __launch_bounds__(512, 1) void stft_kernel(const float* __restrict__ x, int L, int T,
+__global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ x, int L, int T,
                                                       int hop, int pad_mode,
                                                       float* __restrict__ out, MelTab mel) {
   __shared__ __attribute__((aligned(16))) c2 scratch[WAVES * SCR];
   __shared__ c2 qt[QT];
+  __shared__ c2 eht[64];  // W4096^{2 lane + 1}: window phase of the odd samples
   const int b = blockIdx.y;
   const int f0 = blockIdx.x * FR;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   build_qtable(qt);
+  if (threadIdx.x < 64) {
+    double sn, cs;
+    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
+    eht[threadIdx.x] = mk((float)cs, (float)-sn);
+  }
   __syncthreads();
   const float* xr = x + (long long)b * L;
   c2* S = scratch + wave * SCR;
+  float* Sf = reinterpret_cast<float*>(scratch);
+  constexpr int SCRF = 2 * SCR;           // floats per wave scratch
+  float* P = Sf + wave * SCRF + 8 * wave;  // this wave's staged results
+  constexpr int MEL_OFF = 1200;
+  const int nfr = min(FR, T - f0);
 
-  constexpr int NR = (MODE == MODE_MEL) ? 2 : 17;
-  float res[4][NR];
-
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int f = f0 + wave + WAVES * i;
-    if (f < T) {
+#pragma unroll 1
+  for (int r = 0; r < FR / WAVES; ++r) {
+    const int fl = WAVES * r + wave;
+    const int f = f0 + fl;
+    if (fl < nfr) {
       c2 v[16];
-      load_frame(xr, L, f, hop, pad_mode, qt, lane, v);
+      {
+        float2 raw[16];
+        fetch_frame(xr, L, f, hop, pad_mode, lane, raw);
+        const c2 e1 = tw<false>(qt, lane), eh = eht[lane];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = mk(raw[j].x * hann_sq(e1, j), raw[j].y * hann_sq(eh, j));
+      }
       fft1024<false>(v, S, qt, lane);
+      const c2 e1 = tw<false>(qt, lane);  // W2048^lane
       if (MODE == MODE_COMPLEX) {
         float2* o = reinterpret_cast<float2*>(out) + ((long long)b * T + f) * NB;
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          int k = lane + 64 * j;
-          c2 X = post_bin(S, qt, k);
+          const int k = lane + 64 * j;
+          const c2 X = post_bin(S, tw_bin(e1, j), k);
           o[k] = make_float2(X.x, X.y);
         }
         if (lane == 0) {
-          c2 z0 = S[0];
+          const c2 z0 = S[0];
           o[NC] = make_float2(z0.x - z0.y, 0.f);
-        }
-      } else if (MODE == MODE_MEL) {
-        // power spectrum -> this wave's scratch as floats, then 2 bands per lane
-        float P[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          c2 X = post_bin(S, qt, lane + 64 * j);
-          P[j] = X.x * X.x + X.y * X.y;
-        }
-        float pn = 0.f;
-        if (lane == 0) {
-          c2 z0 = S[0];
-          float xn = z0.x - z0.y;
-          pn = xn * xn;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        float* Pf = reinterpret_cast<float*>(S);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) Pf[lane + 64 * j] = P[j];
-        if (lane == 0) Pf[NC] = pn;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          int m = lane + 64 * h;
-          float acc = 0.f;
-          if (m < mel.n_mels) {
-            int s = mel.start[m], n = mel.len[m], wo = mel.woff[m];
-            for (int q = 0; q < n; ++q) acc += mel.w[wo + q] * Pf[s + q];
-          }
-          res[i][h] = acc;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
       } else {
+        float pw[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
-          c2 X = post_bin(S, qt, lane + 64 * j);
-          float p = X.x * X.x + X.y * X.y;
-          res[i][j] = (MODE == MODE_LOGPOW) ? log1p_fast(p) : p;
+          const c2 X = post_bin(S, tw_bin(e1, j), lane + 64 * j);
+          pw[j] = X.x * X.x + X.y * X.y;
         }
-        c2 z0 = S[0];
-        float xn = z0.x - z0.y;
-        float p = xn * xn;
-        res[i][16] = (MODE == MODE_LOGPOW) ? log1p_fast(p) : p;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  if (MODE == MODE_COMPLEX) return;
-
-  // ---- stage through LDS and write (bin, 32-frame) rows ----
-  __syncthreads();
-  float* stage = reinterpret_cast<float*>(scratch);
-  constexpr int SST = FR + 1;
-  const int nfr = min(FR, T - f0);
-  if (MODE == MODE_MEL) {
-    const int nm = mel.n_mels;
+        const c2 z0 = S[0];
+        const float xn = z0.x - z0.y;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int fl = wave + WAVES * i;
+        for (int j = 0; j < 16; ++j)
+          P[lane + 64 * j] = (MODE == MODE_LOGPOW) ? log1p_fast(pw[j]) : pw[j];
+        if (lane == 0) P[NC] = (MODE == MODE_LOGPOW) ? log1p_fast(xn * xn) : xn * xn;
+        if (MODE == MODE_MEL) {
+          // mel bands from the power spectrum (P holds power in MEL mode)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        int m = lane + 64 * h;
-        if (m < nm && fl < nfr) stage[m * SST + fl] = res[i][h];
+          for (int h = 0; h < 2; ++h) {
+            const int m = lane + 64 * h;
+            float acc = 0.f;
+            if (m < mel.n_mels) {
+              const int st = mel.start[m], n = mel.len[m], wo = mel.woff[m];
+              for (int q = 0; q < n; ++q) acc += mel.w[wo + q] * P[st + q];
+            }
+            P[MEL_OFF + m] = acc;
+          }
+        }
       }
     }
+    if (MODE == MODE_COMPLEX) continue;
     __syncthreads();
-    for (int e = threadIdx.x; e < nm * FR; e += blockDim.x) {
-      int m = e / FR, fl = e - m * FR;
-      if (fl < nfr) out[((long long)b * nm + m) * T + f0 + fl] = stage[m * SST + fl];
-    }
-    return;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int fl = wave + WAVES * i;
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        int kr = lane + 64 * jj;  // bin within this round
-        if (fl < nfr) stage[kr * SST + fl] = res[i][4 * r + jj];
-      }
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 256 * FR; e += blockDim.x) {
-      int kr = e / FR, fl = e - kr * FR;
-      if (fl < nfr) out[((long long)b * NB + 256 * r + kr) * T + f0 + fl] = stage[kr * SST + fl];
+    // write round r: frames f0 + 8r .. +7, as (row, 8 frames) runs
+    const int nr = MODE == MODE_MEL ? mel.n_mels : NB;
+    const int roff = MODE == MODE_MEL ? MEL_OFF : 0;
+    const int nfr_r = min(WAVES, nfr - WAVES * r);
+    float* ob = out + (long long)b * nr * T + f0 + WAVES * r;
+    for (int e = threadIdx.x; e < nr * WAVES; e += blockDim.x) {
+      const int k = e >> 3, w = e & 7;
+      if (w < nfr_r) ob[(long long)k * T + w] = Sf[w * SCRF + 8 * w + roff + k];
     }
     __syncthreads();
   }
-  // bin 1024
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int fl = wave + WAVES * i;
-      if (fl < nfr) stage[fl] = res[i][16];
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < nfr) out[((long long)b * NB + NC) * T + f0 + threadIdx.x] = stage[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
@@ -437,6 +440,7 @@ __global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict_
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = wss[i] = 0.f;
   const bool norm = normalize != 0;
+  const c2 e1 = tw<false>(qt, lane);  // W2048^lane
   for (int fb = flo; fb <= fhi; fb += WAVES) {
     const int f = fb + wave;
     if (f <= fhi) {
@@ -453,7 +457,7 @@ __global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict_
         }
         c2 Xc = conj(Xn);
         c2 xe = (Xk + Xc) * 0.5f;
-        c2 xo = cmul(Xk - Xc, tw<true>(qt, k)) * 0.5f;
+        c2 xo = cmul(Xk - Xc, conj(tw_bin(e1, j))) * 0.5f;
         v[j] = xe + mk(-xo.y, xo.x);  // Xe + i Xo
       }
       fft1024<true>(v, S, qt, lane);

@@ -39,6 +39,7 @@ struct GP {
   int M, N, K, nk, splitk;
   long long nA, nP, nx0, nx1;  // elements addressable through each operand descriptor
   int dual;                    // second input source present
+  int nbT, nb0;                // conv: 32-deep K tiles per tap / of source 0 within a tap
   // conv A operand
   const float* A;
   long long sAm, sAc, sAt;
@@ -140,6 +141,16 @@ __device__ __forceinline__ f32x4 ldb4(rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 0));
 }
 
+// voffset (per lane, VGPR) + soffset (wave-uniform, SGPR): the per-element part of a conv
+// operand address is scalar, so these loads cost no VALU.
+__device__ __forceinline__ float ldbs(rsrc_t r, uint32_t voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, soff, 0));
+}
+
+__device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
+}
+
 template <int TAPS, bool WG, int AMODE, bool DUAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
@@ -185,7 +196,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int m = m0 + (AMODE == 2 ? rm_row : km_row + 32 * u);
-      rowA[u] = m < p.M ? (uint32_t)(m * p.sAm) * 4u : OOB;
+      // KM: the lane's k quad is a fixed channel offset within every tile
+      rowA[u] = m < p.M ? (uint32_t)(m * p.sAm + (AMODE == 2 ? 0 : km_kq * p.sAc)) * 4u : OOB;
     }
     const int n = n0 + rm_row;
     const int bb = n / p.Tn;
@@ -210,61 +222,52 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     }
   }
 
-  auto load_tile = [&](int kt) {
+  // Conv K order is tap-major, k = tap * Cp + (source block, channel), each source's channels
+  // padded to a multiple of BK: a 32-deep tile has ONE tap and ONE source, so the tile decode
+  // is scalar, the lane's time index is one VGPR per tile, and every element offset is a
+  // wave-uniform soffset. Padded channels read through a zero-length descriptor (B = 0).
+  const rsrc_t rNull = mk_rsrc(p.x0, 0);
+  auto load_tile = [&](int kt, int tap, int blk) {
     const int k0 = kt * BK;
     if constexpr (!WG) {
+      const bool s1 = DUAL && blk >= p.nb0;
+      const int cb = (s1 ? blk - p.nb0 : blk) * BK;  // first channel of the tile in its source
+      const int ci = cb + (s1 ? p.C0 : 0);           // ... in the concatenated input
+      const int Cs = s1 ? p.C1 : p.C0;
       // ---------------- A ----------------
+      const int sA = (ci * p.sAc + tap * p.sAt) * 4;
       if constexpr (AMODE == 1) {
-        const int k = k0 + km_kq;
-        const uint32_t kb = k < p.K ? (uint32_t)k * 4u : OOB;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const f32x4 v = ldb4(rA, rowA[u] + kb);
+          const f32x4 v = ldbs4(rA, rowA[u], sA);
 #pragma unroll
           for (int i = 0; i < 4; ++i) ra[u][i] = v[i];
         }
       } else if constexpr (AMODE == 0) {
-        uint32_t koff[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int k = k0 + km_kq + i;
-          const int c = k / TAPS;
-          const int tap = k - c * TAPS;
-          koff[i] = k < p.K ? (uint32_t)(c * p.sAc + tap * p.sAt) * 4u : OOB;
-        }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[u][i] = ldb(rA, rowA[u] + koff[i]);
+          for (int i = 0; i < 4; ++i) ra[u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int k = k0 + 4 * (kw + 2 * u) + i;  // wave-uniform
-            const int c = k / TAPS;
-            const int tap = k - c * TAPS;
-            const uint32_t koff = k < p.K ? (uint32_t)(c * p.sAc + tap * p.sAt) * 4u : OOB;
-            ra[u][i] = ldb(rA, rowA[0] + koff);
-          }
+          for (int i = 0; i < 4; ++i)
+            ra[u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
       }
       // ---------------- B: X(b, c, a*t + beta + g*tap), column per lane ----------------
+      const int tin = tinb + p.tg * tap;
+      const int ts = tin + (s1 ? p.off1 : p.off0);
+      const bool ok = ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)(s1 ? p.T1 : p.T0));
+      const uint32_t lo = ok ? (s1 ? colb1 : colb0) + (uint32_t)ts * 4u : OOB;
+      const rsrc_t rB = s1 ? rX1 : rX0;
+      const int scb = (s1 ? p.sc1 : p.sc0) * 4;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int k = k0 + 4 * (kw + 2 * u) + i;  // wave-uniform
-          const int c = k / TAPS;
-          const int tap = k - c * TAPS;
-          const bool s1 = DUAL && c >= p.C0;
-          const int off = s1 ? p.off1 : p.off0;
-          const int Ts = s1 ? p.T1 : p.T0;
-          const uint32_t cb = (uint32_t)(s1 ? (c - p.C0) * p.sc1 : c * p.sc0) * 4u;
-          const int tin = tinb + p.tg * tap;
-          const int ts = tin + off;
-          const bool ok = (k < p.K) & ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)Ts);
-          const uint32_t voff = ok ? (s1 ? colb1 : colb0) + cb + (uint32_t)ts * 4u : OOB;
-          rb[u][i] = ldb(s1 ? rX1 : rX0, voff);
+          const int c = cb + 4 * (kw + 2 * u) + i;  // wave-uniform
+          rb[u][i] = ldbs(c < Cs ? rB : rNull, lo, c * scb);
         }
     } else {
       // wgrad: k = (b, t) per lane (KM)
@@ -341,12 +344,29 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   // end of K every element resolves to the zero block) so no control-flow join forces a
   // vmcnt(0) between the prefetch and this tile's MFMAs.
   if (kt0 < kt1) {
-    load_tile(kt0);
+    int tap = 0, blk = kt0;  // scalar decode of the NEXT tile to load (conv, tap-major K)
+    if constexpr (!WG) {
+      tap = kt0 / p.nbT;
+      blk = kt0 - tap * p.nbT;
+    }
+    auto advance = [&]() {
+      if (++blk == p.nbT) {
+        blk = 0;
+        ++tap;
+      }
+    };
+    load_tile(kt0, tap, blk);
+    advance();
     store_tile(0);
     __syncthreads();
     for (int kt = kt0; kt < kt1; ++kt) {
       const int buf = (kt - kt0) & 1;
-      load_tile(kt + 1);
+      load_tile(kt + 1, tap, blk);
+      advance();
+      // Keep the next tile's global loads at the top of the iteration: left alone, the
+      // scheduler sinks them below the MFMAs, right before the vmcnt wait of store_tile, and
+      // the whole load latency is exposed once per tile.
+      __builtin_amdgcn_sched_barrier(0);
       const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
       const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
 #pragma unroll
@@ -519,17 +539,20 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p = GP{};
   p.M = d->M;
   p.N = d->B * d->Tn;
-  p.K = d->Ctot * d->taps;
-  p.nk = ceil_div(p.K, BK);
   p.A = d->A;
   p.sAm = d->sAm;
   p.sAc = d->sAc;
   p.sAt = d->sAt;
-  const bool kvec = d->sAt == 1 && d->sAc == d->taps && (d->sAm % 4) == 0 && (p.K % 4) == 0 &&
-                    ((uintptr_t)d->A % 16) == 0;
+  fill_src(p, d->src, d->Ctot);
+  // tap-major K with each source's channels padded to whole BK tiles
+  p.nb0 = ceil_div(p.C0, BK);
+  p.nbT = p.nb0 + (p.dual ? ceil_div(p.C1, BK) : 0);
+  p.nk = p.nbT * d->taps;
+  p.K = p.nk * BK;
+  const bool kvec = d->sAc == 1 && (d->sAm % 4) == 0 && (d->taps == 1 || (d->sAt % 4) == 0) &&
+                    (p.C0 % 4) == 0 && ((uintptr_t)d->A % 16) == 0;
   const long long am = d->sAm < 0 ? -d->sAm : d->sAm;
   p.a_mode = kvec ? 1 : (am <= 8 ? 2 : 0);
-  fill_src(p, d->src, d->Ctot);
   p.nA = (long long)(p.M - 1) * d->sAm + (long long)(d->Ctot - 1) * d->sAc +
          (long long)(d->taps - 1) * d->sAt + 1;
   MST_REQUIRE(d->sAm >= 0 && d->sAc >= 0 && d->sAt >= 0);

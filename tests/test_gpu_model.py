@@ -97,10 +97,11 @@ def test_adam_steps_vs_golden(cuda):
         opt.step()
         if step == 2:
             # Adam's first step is sign descent: every gradient element below the fp32 noise
-            # floor moves +-lr at random, so the loss after it carries that noise (ref32 vs
-            # ref64: 1.2e-4 relative). Bound: 1e-3 relative to the fp64 truth.
+            # floor moves +-lr at random, so the loss after it carries that noise. ref32 vs
+            # ref64 is 1.2e-4 relative; two GPU summation orders of the same GEMMs (channel-
+            # major and tap-major K) gave +1.4e-3 and -1.5e-3. Bound: 3e-3 relative to fp64.
             l32, l64 = float(g["loss2"]), float(g["loss2_64"])
-            assert abs(loss.item() - l64) <= max(4 * abs(l32 - l64), 1e-3 * l64), (loss.item(), l32, l64)
+            assert abs(loss.item() - l64) <= max(4 * abs(l32 - l64), 3e-3 * l64), (loss.item(), l32, l64)
         for n, p in net.named_parameters():
             if f"{key}:{n}" not in g.files or _noise_bias(n):
                 continue
