@@ -236,7 +236,7 @@ __device__ __forceinline__ float log1p_fast(float p) {
   float u = 1.f + p;
   float d = u - 1.f;
   float l = __log2f(u) * 0.69314718055994531f;
-  return d == 0.f ? p : l * (p / d);
+  return d == 0.f ? p : l * (p * __builtin_amdgcn_rcpf(d));  // 1-ulp v_rcp, not an IEEE divide
 }
 
 enum { MODE_LOGPOW = 0, MODE_POWER = 1, MODE_MEL = 2, MODE_COMPLEX = 3 };
@@ -283,7 +283,7 @@ __device__ __forceinline__ void fetch_frame(const float* xr, int L, int f, int h
 
 // STFT: 512 threads = 8 waves, 32 frames per workgroup in 4 rounds of 8 (one frame per wave).
 // Twiddles and window values come from one per-lane table lookup times compile-time roots of
-// unity (see twiddle_powers / tw_bin / hann_ej); each wave leaves its frame's 1025 results in its own LDS scratch (offset by
+// unity (see twiddle_powers / tw_bin / hann_sq); each wave leaves its frame's 1025 results in its own LDS scratch (offset by
 // 8 floats per wave so the transposed read is bank-conflict-free), and after a barrier the
 // workgroup writes the round as (bin, 8 frames) runs of the frequency-major (B, F, T) output.
 // 73.7 KB LDS per workgroup.
@@ -409,8 +409,8 @@ __device__ __forceinline__ c2 gl_bin(const float2* cur, const float2* prev, cons
     a = a - mk(pv.x, pv.y) * beta;
   }
   if (normalize) {
-    float n = sqrtf(a.x * a.x + a.y * a.y) + 1e-16f;
-    a = mk(a.x / n, a.y / n);
+    const float inv = __builtin_amdgcn_rcpf(sqrtf(a.x * a.x + a.y * a.y) + 1e-16f);
+    a = mk(a.x * inv, a.y * inv);
   }
   if (mag) a = a * mag[base + k];
   return a;

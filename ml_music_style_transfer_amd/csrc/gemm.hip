@@ -25,6 +25,8 @@
 // shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
 // every loader VALU instruction costs MFMA issue time: the per-element index work is kept
 // wave-uniform (scalar) wherever the mapping allows it.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -129,6 +131,13 @@ __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) 
   *o = v;
 }
 
+// Value select: `c ? x : y` on two lvalues (lambda captures, kernarg fields) is an lvalue, and
+// the compiler implements it by taking both addresses, which moves the operands to scratch.
+template <class T>
+__device__ __forceinline__ T sel(bool c, T x, T y) {
+  return c ? x : y;
+}
+
 __device__ __forceinline__ rsrc_t mk_rsrc(const float* ptr, long long n) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)ptr, (short)0, (int)(n * 4), 0x00020000);
 }
@@ -177,7 +186,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int rm_row = tid & 127;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 7);
 
-  float ra[4][4], rb[4][4];
+  float ra[2][4][4], rb[2][4][4];  // two register stages: tile k+2 loads while k+1 waits
 
   // ------------------------------------------------------------ loaders
   const rsrc_t rX0 = mk_rsrc(p.x0, p.nx0);
@@ -226,14 +235,14 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   // padded to a multiple of BK: a 32-deep tile has ONE tap and ONE source, so the tile decode
   // is scalar, the lane's time index is one VGPR per tile, and every element offset is a
   // wave-uniform soffset. Padded channels read through a zero-length descriptor (B = 0).
-  const rsrc_t rNull = mk_rsrc(p.x0, 0);
-  auto load_tile = [&](int kt, int tap, int blk) {
+  auto load_tile = [&](auto S, int kt, int tap, int blk) __attribute__((always_inline)) {
+    constexpr int st = decltype(S)::value;
     const int k0 = kt * BK;
     if constexpr (!WG) {
       const bool s1 = DUAL && blk >= p.nb0;
       const int cb = (s1 ? blk - p.nb0 : blk) * BK;  // first channel of the tile in its source
-      const int ci = cb + (s1 ? p.C0 : 0);           // ... in the concatenated input
-      const int Cs = s1 ? p.C1 : p.C0;
+      const int ci = cb + sel(s1, p.C0, 0);           // ... in the concatenated input
+      const int Cs = sel(s1, p.C1, p.C0);
       // ---------------- A ----------------
       const int sA = (ci * p.sAc + tap * p.sAt) * 4;
       if constexpr (AMODE == 1) {
@@ -241,33 +250,35 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
         for (int u = 0; u < 4; ++u) {
           const f32x4 v = ldbs4(rA, rowA[u], sA);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[u][i] = v[i];
+          for (int i = 0; i < 4; ++i) ra[st][u][i] = v[i];
         }
       } else if constexpr (AMODE == 0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
+          for (int i = 0; i < 4; ++i) ra[st][u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            ra[u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
+            ra[st][u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
       }
       // ---------------- B: X(b, c, a*t + beta + g*tap), column per lane ----------------
       const int tin = tinb + p.tg * tap;
-      const int ts = tin + (s1 ? p.off1 : p.off0);
-      const bool ok = ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)(s1 ? p.T1 : p.T0));
-      const uint32_t lo = ok ? (s1 ? colb1 : colb0) + (uint32_t)ts * 4u : OOB;
-      const rsrc_t rB = s1 ? rX1 : rX0;
-      const int scb = (s1 ? p.sc1 : p.sc0) * 4;
+      const int ts = tin + sel(s1, p.off1, p.off0);
+      const bool ok = ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)sel(s1, p.T1, p.T0));
+      const uint32_t lo = ok ? sel(s1, colb1, colb0) + (uint32_t)ts * 4u : OOB;
+      // source descriptor built from scalars (selecting between descriptors spills them)
+      const float* xs = sel(DUAL && s1, p.x1, p.x0);
+      const long long ns = sel(DUAL && s1, p.nx1, p.nx0);
+      const int scb = sel(s1, p.sc1, p.sc0) * 4;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = cb + 4 * (kw + 2 * u) + i;  // wave-uniform
-          rb[u][i] = ldbs(c < Cs ? rB : rNull, lo, c * scb);
+          rb[st][u][i] = ldbs(mk_rsrc(xs, c < Cs ? ns : 0), lo, c * scb);
         }
     } else {
       // wgrad: k = (b, t) per lane (KM)
@@ -288,7 +299,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[u][i] = ldb(rA, rowA[u] + kP[i]);
+        for (int i = 0; i < 4; ++i) ra[st][u][i] = ldb(rA, rowA[u] + kP[i]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -300,20 +311,21 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
           if constexpr (DUAL) {
             const float v0 = ldb(rX0, ok && !nsel1[u] ? base + kb0[i] : OOB);
             const float v1 = ldb(rX1, ok && nsel1[u] ? base + kb1[i] : OOB);
-            rb[u][i] = v0 + v1;
+            rb[st][u][i] = v0 + v1;
           } else {
-            rb[u][i] = ldb(rX0, ok ? base + kb0[i] : OOB);
+            rb[st][u][i] = ldb(rX0, ok ? base + kb0[i] : OOB);
           }
         }
     }
   };
 
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
+    constexpr int st = decltype(S)::value;
     float* As = lds[buf];
     float* Bs = lds[buf] + BM * LDK;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 v = {ra[u][0], ra[u][1], ra[u][2], ra[u][3]};
+      f32x4 v = {ra[st][u][0], ra[st][u][1], ra[st][u][2], ra[st][u][3]};
       if constexpr (AMODE == 2 && !WG)
         *reinterpret_cast<f32x4*>(As + rm_row * LDK + (kw + 2 * u) * 4) = v;
       else
@@ -321,7 +333,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 v = {rb[u][0], rb[u][1], rb[u][2], rb[u][3]};
+      f32x4 v = {rb[st][u][0], rb[st][u][1], rb[st][u][2], rb[st][u][3]};
       if constexpr (WG)
         *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
       else
@@ -343,48 +355,62 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   // Branch-free main loop: the prefetch of tile k+1 is issued unconditionally (past the
   // end of K every element resolves to the zero block) so no control-flow join forces a
   // vmcnt(0) between the prefetch and this tile's MFMAs.
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
+    const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
+    const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f32x4 a0 = *reinterpret_cast<const f32x4*>(As + g * 4);
+      f32x4 a1 = *reinterpret_cast<const f32x4*>(As + 32 * LDK + g * 4);
+      f32x4 b0 = *reinterpret_cast<const f32x4*>(Bs + g * 4);
+      f32x4 b1 = *reinterpret_cast<const f32x4*>(Bs + 32 * LDK + g * 4);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
+      }
+    }
+  };
+
+  // Pipeline: LDS double buffer + two register stages. Iteration k issues the global loads of
+  // tile k+2, runs tile k's MFMAs from LDS, then stores tile k+1 (loaded one iteration
+  // earlier, so its latency is covered by a full tile of MFMAs) into the other LDS buffer.
+  // Loads past the end are harmless (bounded buffer loads) and never consumed.
   if (kt0 < kt1) {
     int tap = 0, blk = kt0;  // scalar decode of the NEXT tile to load (conv, tap-major K)
     if constexpr (!WG) {
       tap = kt0 / p.nbT;
       blk = kt0 - tap * p.nbT;
     }
-    auto advance = [&]() {
+    auto advance = [&]() __attribute__((always_inline)) {
       if (++blk == p.nbT) {
         blk = 0;
         ++tap;
       }
     };
-    load_tile(kt0, tap, blk);
+    load_tile(I0{}, kt0, tap, blk);
     advance();
-    store_tile(0);
+    load_tile(I1{}, kt0 + 1, tap, blk);
+    advance();
+    store_tile(I0{}, 0);
     __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int buf = (kt - kt0) & 1;
-      load_tile(kt + 1, tap, blk);
+    auto step = [&](auto S, int kt) __attribute__((always_inline)) {
+      constexpr int sb = decltype(S)::value;
+      load_tile(S, kt + 2, tap, blk);
       advance();
-      // Keep the next tile's global loads at the top of the iteration: left alone, the
-      // scheduler sinks them below the MFMAs, right before the vmcnt wait of store_tile, and
-      // the whole load latency is exposed once per tile.
+      // keep the loads above the MFMAs (the scheduler would otherwise sink them)
       __builtin_amdgcn_sched_barrier(0);
-      const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
-      const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(As + g * 4);
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(As + 32 * LDK + g * 4);
-        f32x4 b0 = *reinterpret_cast<const f32x4*>(Bs + g * 4);
-        f32x4 b1 = *reinterpret_cast<const f32x4*>(Bs + 32 * LDK + g * 4);
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
-        }
-      }
-      store_tile(buf ^ 1);
+      mfma_tile(sb);
+      store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
+    };
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      step(I0{}, kt);
+      if (kt + 1 < kt1) step(I1{}, kt + 1);
     }
   }
 
