@@ -381,15 +381,20 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   // earlier, so its latency is covered by a full tile of MFMAs) into the other LDS buffer.
   // Loads past the end are harmless (bounded buffer loads) and never consumed.
   if (kt0 < kt1) {
-    int tap = 0, blk = kt0;  // scalar decode of the NEXT tile to load (conv, tap-major K)
-    if constexpr (!WG) {
-      tap = kt0 / p.nbT;
-      blk = kt0 - tap * p.nbT;
+    // scalar decode of the NEXT tile to load (conv: tap, source block)
+    constexpr bool DECODE = !WG;
+    const int per = p.nbT;
+    int tap = 0, blk = kt0;
+    if constexpr (DECODE) {
+      tap = kt0 / per;
+      blk = kt0 - tap * per;
     }
     auto advance = [&]() __attribute__((always_inline)) {
-      if (++blk == p.nbT) {
-        blk = 0;
-        ++tap;
+      if constexpr (DECODE) {
+        if (++blk == per) {
+          blk = 0;
+          ++tap;
+        }
       }
     };
     load_tile(I0{}, kt0, tap, blk);
