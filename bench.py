@@ -201,6 +201,15 @@ def main():
     gemm_flops = sum(ev[2] for ev in log)
     n_steps_t = max(1, args.kernel_timing_steps)
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    # algorithmic bytes per GEMM launch: each operand and the output once, (MK + KN + MN) x 4
+    alg_bytes = [4.0 * (shp[0] * shp[2] + shp[2] * shp[1] + shp[0] * shp[1]) for *_, shp in log if shp]
+    traffic, traffic_src = None, None
+    tj = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
+    if os.path.exists(tj):
+        with open(tj) as fh:
+            traffic = round(json.load(fh)["traffic_bytes_per_launch"])
+        traffic_src = ("profiles/r01/gemm_traffic.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
+                       "passes over this bench, 2 x fetch + write per gemm_kernel launch")
     by_tag = {}
     for s, e, f, tag, _ in log:
         a = by_tag.setdefault(tag, [0.0, 0.0, 0])
@@ -232,10 +241,13 @@ def main():
             "peak": PEAK_FP32_MFMA,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP32_MFMA, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": round(sum(alg_bytes) / max(len(alg_bytes), 1)),
             "gemm_gflop_per_step": round(gemm_flops / n_steps_t / 1e9, 1),
             "gemm_ms_per_step": round(gemm_ms / n_steps_t, 3),
             "launches_per_step": len(log) // n_steps_t,
+            "avg_launch_ms": round(gemm_ms / max(len(log), 1), 4),
             "by_kind": {k: {"ms_per_step": round(v[0] / n_steps_t, 3),
                             "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] else 0}
                         for k, v in by_tag.items()},

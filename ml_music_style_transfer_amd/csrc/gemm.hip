@@ -168,9 +168,23 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * BN;
-  const int m0 = blockIdx.y * BM;
-  const int split = blockIdx.z;
+  // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear id % 8),
+  // each with its own L2. Renumber so every XCD runs one contiguous range of tiles, N fastest:
+  // the workgroups that share an A panel (one M tile, all N tiles) then sit on one XCD and
+  // read it through one L2 instead of eight.
+  int n_t, m_t, split;
+  {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int W = nx * ny * (int)gridDim.z;
+    const int w = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+    const int q = W >> 3, r = W & 7, xcd = w & 7;
+    const int t = xcd * q + min(xcd, r) + (w >> 3);
+    n_t = t % nx;
+    m_t = (t / nx) % ny;
+    split = t / (nx * ny);
+  }
+  const int n0 = n_t * BN;
+  const int m0 = m_t * BM;
   const int kt0 = (int)((long long)split * p.nk / p.splitk);
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
 
