@@ -34,6 +34,7 @@ namespace {
 constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256, LDK = BK + 4;
 
 constexpr uint32_t OOB = 0x7FFFFFF0u;  // byte offset past every descriptor's num_records
+constexpr int MAXCLS = 8;              // wgrad K classes
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
@@ -50,7 +51,9 @@ struct GP {
   const float* P;
   long long sPb;
   int sPc, Tk;
-  float invTk;
+  int Tp, lo, span;  // padded time axis; valid input times [lo, lo + span) of the single source
+  int ncls;          // K classes of the wgrad tile order (see the main loop)
+  int cstart[MAXCLS + 1], ct0[MAXCLS], ccnt[MAXCLS], cmask[MAXCLS];
   // virtual input (B operand source)
   const float* x0;
   long long sb0;
@@ -85,14 +88,6 @@ struct GP {
   // split-K slab
   float* ws;
 };
-
-// q = k / d, r = k % d for 0 <= k < 2^24 via a float reciprocal and one correction step.
-__device__ __forceinline__ void divmod_f(int k, int d, float inv, int& q, int& r) {
-  q = (int)((float)k * inv);
-  r = k - q * d;
-  if (r < 0) { --q; r += d; }
-  else if (r >= d) { ++q; r -= d; }
-}
 
 __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
   if (m >= p.M || n >= p.N) return;
@@ -200,21 +195,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int rm_row = tid & 127;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 7);
 
-  float ra[2][4][4], rb[2][4][4];  // two register stages: tile k+2 loads while k+1 waits
+  f32x4 ra[2][4], rb[2][4];  // two register stages: tile k+2 loads while k+1 waits
 
   // ------------------------------------------------------------ loaders
   const rsrc_t rX0 = mk_rsrc(p.x0, p.nx0);
-  const rsrc_t rX1 = mk_rsrc(DUAL ? p.x1 : p.x0, DUAL ? p.nx1 : 0);
   const rsrc_t rA = mk_rsrc(WG ? p.P : p.A, WG ? p.nP : p.nA);
 
   // per-lane constants
   uint32_t rowA[4];
   int tinb = 0;
   uint32_t colb0 = 0, colb1 = 0;
-  // wgrad B rows
-  uint32_t rowX[4];
-  int gtb[4], offs[4], Tsrc[4];
-  bool nsel1[4];
+  // wgrad: per-element offsets of the current K class (set per class, see the main loop)
+  uint32_t vA[4], vB[4][4];
+  int tlb = 0, bdl = 0;
   if constexpr (!WG) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -229,29 +222,50 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     colb0 = (uint32_t)(bb * p.sb0) * 4u;
     colb1 = DUAL ? (uint32_t)(bb * p.sb1) * 4u : 0u;
   } else {
+    // wgrad K order: k = (b, t) with the time axis padded to Tp (16, or a multiple of 32), so
+    // a 32-deep tile is one batch row (or two 16-halves when Tp = 16). The lane's k quad (4
+    // consecutive t) sits at time tlb of batch b + bdl.
+    const int q = tid & 7;
+    tlb = 4 * q;
+    if (p.Tp == 16 && q >= 4) {
+      tlb -= 16;
+      bdl = 1;
+    }
+  }
+  // Per-element offsets of one wgrad K class: every tile of the class shares the time offset
+  // t0 - t0ref (a scalar soffset), so range checks against the input and the padding are
+  // evaluated once per class here and the tile loop has no per-element work. Invalid elements
+  // get the OOB offset (hardware zero).
+  auto wg_class_setup = [&](int t0ref, bool masked) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int m = m0 + km_row + 32 * u;
-      rowA[u] = m < p.M ? (uint32_t)(m * p.sPc) * 4u : OOB;
       const int n = n0 + km_row + 32 * u;
       const int c = n / TAPS;
       const int tap = n - c * TAPS;
-      const bool s1 = DUAL && c >= p.C0;
-      nsel1[u] = s1;
-      rowX[u] = (uint32_t)(s1 ? (c - p.C0) * p.sc1 : c * p.sc0) * 4u;
-      gtb[u] = n < p.N ? p.tb + p.tg * tap : -(1 << 29);
-      offs[u] = s1 ? p.off1 : p.off0;
-      Tsrc[u] = s1 ? p.T1 : p.T0;
+      const int abase = m * p.sPc + bdl * (int)p.sPb + t0ref + tlb;
+      const int tin0 = p.ta * (t0ref + tlb) + p.tb + p.tg * tap;  // input time at i = 0
+      const int bbase = c * p.sc0 + bdl * (int)p.sb0 + tin0 + p.off0;
+      // A (P) is read unmasked: padded times read finite neighbours (or OOB zeros) and are
+      // multiplied by B elements masked to zero there.
+      vA[u] = m < p.M ? (uint32_t)abase * 4u : OOB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tin = tin0 + p.ta * i;
+        const bool bok = n < p.N && (!masked || ((unsigned)(tin - p.lo) < (unsigned)p.span &&
+                                                 t0ref + tlb + i < p.Tk));
+        vB[u][i] = bok ? (uint32_t)(bbase + p.ta * i) * 4u : OOB;
+      }
     }
-  }
+  };
 
   // Conv K order is tap-major, k = tap * Cp + (source block, channel), each source's channels
   // padded to a multiple of BK: a 32-deep tile has ONE tap and ONE source, so the tile decode
   // is scalar, the lane's time index is one VGPR per tile, and every element offset is a
   // wave-uniform soffset. Padded channels read through a zero-length descriptor (B = 0).
   auto load_tile = [&](auto S, int kt, int tap, int blk) __attribute__((always_inline)) {
-    constexpr int st = decltype(S)::value;
-    const int k0 = kt * BK;
+    constexpr int st_ = decltype(S)::value;
+    (void)kt;
     if constexpr (!WG) {
       const bool s1 = DUAL && blk >= p.nb0;
       const int cb = (s1 ? blk - p.nb0 : blk) * BK;  // first channel of the tile in its source
@@ -262,21 +276,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
       if constexpr (AMODE == 1) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const f32x4 v = ldbs4(rA, rowA[u], sA);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) ra[st][u][i] = v[i];
+          ra[st_][u] = ldbs4(rA, rowA[u], sA);
         }
       } else if constexpr (AMODE == 0) {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ra[st][u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
+          for (int i = 0; i < 4; ++i) ra[st_][u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
       } else {
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            ra[st][u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
+            ra[st_][u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
       }
       // ---------------- B: X(b, c, a*t + beta + g*tap), column per lane ----------------
       const int tin = tinb + p.tg * tap;
@@ -292,44 +304,20 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = cb + 4 * (kw + 2 * u) + i;  // wave-uniform
-          rb[st][u][i] = ldbs(mk_rsrc(xs, c < Cs ? ns : 0), lo, c * scb);
+          rb[st_][u][i] = ldbs(mk_rsrc(xs, c < Cs ? ns : 0), lo, c * scb);
         }
     } else {
-      // wgrad: k = (b, t) per lane (KM)
-      const int k = k0 + km_kq;
-      uint32_t kP[4], kb0[4], kb1[4];
-      int ta_t[4];
-      bool kok[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        int b, t;
-        divmod_f(k + i, p.Tk, p.invTk, b, t);
-        kok[i] = (k + i) < p.K;
-        kP[i] = kok[i] ? (uint32_t)(b * p.sPb + t) * 4u : OOB;
-        kb0[i] = (uint32_t)(b * p.sb0) * 4u;
-        kb1[i] = DUAL ? (uint32_t)(b * p.sb1) * 4u : 0u;
-        ta_t[i] = kok[i] ? p.ta * t : -(1 << 29);
-      }
+      // wgrad tile of batch row b = tap at time t0ref + 32 * blk: one scalar soffset per operand
+      const int sA = (tap * (int)p.sPb + BK * blk) * 4;
+      const int sB = (tap * (int)p.sb0 + p.ta * BK * blk) * 4;
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[st][u][i] = ldb(rA, rowA[u] + kP[i]);
+        for (int i = 0; i < 4; ++i) ra[st_][u][i] = ldbs(rA, vA[u], sA + 4 * i);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int tin = ta_t[i] + gtb[u];
-          const int ts = tin + offs[u];
-          const bool ok = (unsigned)tin < (unsigned)p.Tv && (unsigned)ts < (unsigned)Tsrc[u];
-          const uint32_t base = rowX[u] + (uint32_t)ts * 4u;
-          if constexpr (DUAL) {
-            const float v0 = ldb(rX0, ok && !nsel1[u] ? base + kb0[i] : OOB);
-            const float v1 = ldb(rX1, ok && nsel1[u] ? base + kb1[i] : OOB);
-            rb[st][u][i] = v0 + v1;
-          } else {
-            rb[st][u][i] = ldb(rX0, ok ? base + kb0[i] : OOB);
-          }
-        }
+        for (int i = 0; i < 4; ++i) rb[st_][u][i] = ldbs(rX0, vB[u][i], sB);
     }
   };
 
@@ -339,7 +327,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     float* Bs = lds[buf] + BM * LDK;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 v = {ra[st][u][0], ra[st][u][1], ra[st][u][2], ra[st][u][3]};
+      const f32x4 v = ra[st][u];
       if constexpr (AMODE == 2 && !WG)
         *reinterpret_cast<f32x4*>(As + rm_row * LDK + (kw + 2 * u) * 4) = v;
       else
@@ -347,7 +335,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      f32x4 v = {rb[st][u][0], rb[st][u][1], rb[st][u][2], rb[st][u][3]};
+      const f32x4 v = rb[st][u];
       if constexpr (WG)
         *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
       else
@@ -394,26 +382,19 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   // tile k+2, runs tile k's MFMAs from LDS, then stores tile k+1 (loaded one iteration
   // earlier, so its latency is covered by a full tile of MFMAs) into the other LDS buffer.
   // Loads past the end are harmless (bounded buffer loads) and never consumed.
-  if (kt0 < kt1) {
-    // scalar decode of the NEXT tile to load (conv: tap, source block)
-    constexpr bool DECODE = !WG;
-    const int per = p.nbT;
-    int tap = 0, blk = kt0;
-    if constexpr (DECODE) {
-      tap = kt0 / per;
-      blk = kt0 - tap * per;
-    }
+  // run(): one pipelined pass over tiles [kb, ke) starting at scalar decode (tap, blk).
+  //   conv : (tap, source block) of a tap-major K
+  //   wgrad: (batch row b, tile index j within the class), `per` tiles per row
+  auto run = [&](int kb, int ke, int tap, int blk, int per) __attribute__((always_inline)) {
     auto advance = [&]() __attribute__((always_inline)) {
-      if constexpr (DECODE) {
-        if (++blk == per) {
-          blk = 0;
-          ++tap;
-        }
+      if (++blk == per) {
+        blk = 0;
+        tap += (WG && p.Tp == 16) ? 2 : 1;
       }
     };
-    load_tile(I0{}, kt0, tap, blk);
+    load_tile(I0{}, kb, tap, blk);
     advance();
-    load_tile(I1{}, kt0 + 1, tap, blk);
+    load_tile(I1{}, kb + 1, tap, blk);
     advance();
     store_tile(I0{}, 0);
     __syncthreads();
@@ -427,9 +408,27 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
       store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
     };
-    for (int kt = kt0; kt < kt1; kt += 2) {
+    for (int kt = kb; kt < ke; kt += 2) {
       step(I0{}, kt);
-      if (kt + 1 < kt1) step(I1{}, kt + 1);
+      if (kt + 1 < ke) step(I1{}, kt + 1);
+    }
+  };
+  if constexpr (!WG) {
+    if (kt0 < kt1) {
+      const int tap = kt0 / p.nbT;
+      run(kt0, kt1, tap, kt0 - tap * p.nbT, p.nbT);
+    }
+  } else {
+    // K classes (host-built): tiles [cstart[c], cstart[c+1]) are (b, j) row-major with
+    // ccnt[c] tiles per row at times ct0[c] + 32 j; boundary classes have ccnt = 1.
+    for (int c = 0; c < p.ncls; ++c) {
+      const int kb = max(kt0, p.cstart[c]);
+      const int ke = min(kt1, p.cstart[c + 1]);
+      if (kb >= ke) continue;
+      wg_class_setup(p.ct0[c], p.cmask[c] != 0);
+      const int rel = kb - p.cstart[c];
+      const int row = rel / p.ccnt[c];
+      run(kb, ke, (p.Tp == 16 ? 2 : 1) * row, rel - row * p.ccnt[c], p.ccnt[c]);
     }
   }
 
@@ -510,8 +509,8 @@ int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   dim3 block(NTHR);
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
-  if (p.dual)                                                                        \
-    hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, true>), grid, block, 0, st, p);      \
+  if (!WG && p.dual)                                                                 \
+    hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, !WG>), grid, block, 0, st, p);       \
   else                                                                               \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, false>), grid, block, 0, st, p);
 #define MST_GEMM_CASE(TP)                                                            \
@@ -633,33 +632,80 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   return MST_OK;
 }
 
-int build_wgrad(const mst_wgrad_desc* d, GP& p) {
-  MST_REQUIRE(d && d->P && d->src[0].p && d->out);
-  MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tk > 0 && d->Ctot > 0 && taps_ok(d->taps));
-  MST_REQUIRE(d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
+// Weight-gradient GEMM over ONE input source (a virtual concat is split into one launch per
+// source by the caller): columns [0, C*taps) of `out` for that source's channels.
+int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) {
+  MST_REQUIRE(d && d->P && src.p && out);
+  MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tk > 0 && src.C > 0 && taps_ok(d->taps));
+  MST_REQUIRE(d->g >= 0 && d->a >= 1);
   p = GP{};
   p.M = d->M;
-  p.N = d->Ctot * d->taps;
-  p.K = d->B * d->Tk;
-  p.nk = ceil_div(p.K, BK);
+  p.N = src.C * d->taps;
+  // time axis padded to Tp: 16 for short rows, else a multiple of BK (a tile = one batch row)
+  p.Tp = d->Tk <= 16 ? 16 : ceil_div(d->Tk, BK) * BK;
   p.P = d->P;
   p.sPb = d->sPb;
   p.sPc = d->sPc;
   p.Tk = d->Tk;
-  p.invTk = 1.0f / (float)d->Tk;
-  fill_src(p, d->src, d->Ctot);
+  mst_src one[2] = {src, mst_src{}};
+  fill_src(p, one, src.C);
   p.nP = (long long)(d->B - 1) * d->sPb + (long long)(d->M - 1) * d->sPc + d->Tk;
   MST_REQUIRE(src_extent(p, d->B) == MST_OK && p.nP * 4 < (long long)OOB);
+  MST_REQUIRE(p.sPb * 2 < (long long)OOB / 4);
   p.Tv = d->Tv;
   p.ta = d->a;
   p.tb = d->beta;
   p.tg = d->g;
-  p.out = d->out;
+  // valid input times: 0 <= tin < Tv and 0 <= tin + off < T
+  const int lo = src.off < 0 ? -src.off : 0;
+  const int hi = d->Tv < src.T - src.off ? d->Tv : src.T - src.off;
+  p.lo = lo;
+  p.span = hi > lo ? hi - lo : 0;
+  // K classes: per time tile j (t0 = 32 j) of a batch row, "interior" when every element of
+  // every row is in range; consecutive interior tiles share one unmasked class, every other
+  // tile is a masked class of its own (ranges are monotone in t0, so there are few).
+  const int rows = p.Tp == 16 ? ceil_div(d->B, 2) : d->B;
+  const int nj = p.Tp == 16 ? 1 : p.Tp / BK;
+  p.ncls = 0;
+  int start = 0;
+  for (int j = 0; j < nj;) {
+    const int t0 = BK * j;
+    auto interior = [&](int t) {
+      const int st = d->a * t + d->beta;
+      return t + BK <= d->Tk && st >= p.lo && st + d->a * (BK - 1) + d->g * (d->taps - 1) < p.lo + p.span;
+    };
+    int cnt = 1;
+    const bool in = interior(t0);
+    if (in)
+      while (j + cnt < nj && interior(BK * (j + cnt))) ++cnt;
+    MST_REQUIRE(p.ncls < MAXCLS);
+    p.cstart[p.ncls] = start;
+    p.ct0[p.ncls] = t0;
+    p.ccnt[p.ncls] = cnt;
+    p.cmask[p.ncls] = in ? 0 : 1;
+    ++p.ncls;
+    start += rows * cnt;
+    j += cnt;
+  }
+  p.cstart[p.ncls] = start;
+  p.nk = start;
+  p.K = p.nk * BK;
+  p.out = out;
   p.ldo = d->ldo;
   p.scale = d->scale;
   p.accumulate = d->accumulate;
   p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
   return MST_OK;
+}
+
+int wgrad_sources(const mst_wgrad_desc* d, mst_src* srcs, float** outs) {
+  MST_REQUIRE(d && d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
+  srcs[0] = d->src[0];
+  outs[0] = d->out;
+  if (d->src[1].C <= 0) return 1;
+  srcs[1] = d->src[1];
+  outs[1] = d->out + (long long)d->src[0].C * d->taps;
+  return 2;
 }
 
 }  // namespace
@@ -685,21 +731,43 @@ int mst_conv_fwd_f32(const mst_conv_desc* d, float* ws, size_t ws_bytes, void* s
 }
 
 size_t mst_wgrad_workspace_size(const mst_wgrad_desc* d) {
-  GP p;
-  if (build_wgrad(d, p) != MST_OK) return 0;
-  return p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+  mst_src srcs[2];
+  float* outs[2];
+  if (!d) return 0;
+  const int ns = wgrad_sources(d, srcs, outs);
+  if (ns < 1) return 0;
+  size_t need = 0;
+  for (int i = 0; i < ns; ++i) {
+    GP p;
+    if (build_wgrad(d, srcs[i], outs[i], p) != MST_OK) return 0;
+    const size_t w = p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+    need = w > need ? w : need;
+  }
+  return need;
 }
 
 int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* ws, size_t ws_bytes, void* stream) {
-  GP p;
-  int rc = build_wgrad(d, p);
-  if (rc) return rc;
-  if (p.splitk > 1) {
-    size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
-    if (!ws || ws_bytes < need) p.splitk = 1;
-    p.ws = ws;
+  mst_src srcs[2];
+  float* outs[2];
+  if (!d) return MST_EINVAL;
+  const int ns = wgrad_sources(d, srcs, outs);
+  if (ns < 1) return MST_EINVAL;
+  GP ps[2];
+  for (int i = 0; i < ns; ++i) {  // validate every launch before enqueueing any
+    int rc = build_wgrad(d, srcs[i], outs[i], ps[i]);
+    if (rc) return rc;
   }
-  return launch<true>(p, (hipStream_t)stream, d->taps);
+  for (int i = 0; i < ns; ++i) {
+    GP& p = ps[i];
+    if (p.splitk > 1) {
+      size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
+      if (!ws || ws_bytes < need) p.splitk = 1;
+      p.ws = ws;
+    }
+    int rc = launch<true>(p, (hipStream_t)stream, d->taps);
+    if (rc) return rc;
+  }
+  return MST_OK;
 }
 
 }  // extern "C"

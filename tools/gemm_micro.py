@@ -1,0 +1,69 @@
+"""GEMM microbenchmark: one conv3 layer's fwd / dgrad / wgrad launched back to back (dev tool).
+
+usage: python tools/gemm_micro.py [--B 32] [--T 126] [--cin 2048] [--cout 2048] [--reps 20]
+                                  [--kinds fwd,dgrad,wgrad]
+Prints TF/s per kind (HIP events on the launch stream). Short enough to run under
+rocprofv3 --pmc passes.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--B", type=int, default=32)
+    ap.add_argument("--T", type=int, default=126)
+    ap.add_argument("--cin", type=int, default=2048)
+    ap.add_argument("--cout", type=int, default=2048)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--kinds", default="fwd,dgrad,wgrad")
+    ap.add_argument("--layer", default="conv3", choices=["conv3", "linear"])
+    args = ap.parse_args()
+    from ml_music_style_transfer_amd import kernels as K
+
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    B, T, Ci, Co = args.B, args.T, args.cin, args.cout
+    taps = 3 if args.layer == "conv3" else 1
+    x = torch.randn(B, Ci, T, device=dev, generator=g)
+    W = torch.randn(Co, Ci, taps, device=dev, generator=g) * 0.02 if taps == 3 else \
+        torch.randn(Co, Ci, device=dev, generator=g) * 0.02
+    bias = torch.zeros(Co, device=dev)
+    y = torch.empty(B, Co, T, device=dev)
+    dy = torch.randn(B, Co, T, device=dev, generator=g)
+    dx = torch.empty_like(x)
+    dW = torch.empty_like(W)
+    flops = 2.0 * B * T * Ci * Co * taps
+    fns = {
+        "conv3": {"fwd": lambda: K.conv3_fwd([(x, 0)], W, bias, y),
+                  "dgrad": lambda: K.conv3_dgrad(dy, W, [(dx, 0, None, 1.0)]),
+                  "wgrad": lambda: K.conv3_wgrad(dy, [(x, 0)], dW, False)},
+        "linear": {"fwd": lambda: K.linear_fwd([(x, 0)], W, bias, y),
+                   "dgrad": lambda: K.linear_dgrad(dy, W, [(dx, 0, None, 1.0)]),
+                   "wgrad": lambda: K.linear_wgrad(dy, [(x, 0)], dW, False)},
+    }[args.layer]
+    for kind in args.kinds.split(","):
+        fn = fns[kind]
+        for _ in range(3):
+            fn()
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(args.reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / args.reps
+        print(f"{args.layer} {kind:6s} B={B} T={T} Cin={Ci} Cout={Co}: {ms:.4f} ms "
+              f"{flops / ms / 1e9:.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

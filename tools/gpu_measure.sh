@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU-box measurement pass (run via gpurun from the repo root). Each GPU step has its own
+# time limit and the steps are chained: the first failure ends the script.
+#   tools/gpu_measure.sh TAG [tests] [bench] [prof] [pmc] [aux]
+set -e -o pipefail
+TAG=${1:?tag}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+for what in "$@"; do
+  case $what in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        > "$OUT/pytest_gpu.log" 2>&1 ;;
+    bench)
+      timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" ;;
+    pmc)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_fetch.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_write.log" 2>&1 ;;
+    aux)
+      timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
+    layers)
+      timeout -k 10 300 python -u tools/gemm_layers.py > "$OUT/gemm_layers.txt" 2> "$OUT/gemm_layers.err" ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
+    *) echo "unknown step $what"; exit 2 ;;
+  esac
+  echo "step $what ok"
+done
