@@ -98,9 +98,10 @@ typedef struct mst_conv_desc {
 } mst_conv_desc;
 
 /* Weight gradient of a conv-like layer:
- *   W[m][c*taps + tap] (+)= scale * sum_{b,t} P[b][m][t] * X(b, c, a*t + beta + g*tap)
+ *   out[m*ldo + c*ldc + tap*ldt] (+)= scale * sum_{b,t} P[b][m][t] * X(b, c, a*t + beta + g*tap)
  * P: (B, M, Tk) NCL (contiguous in t), X: virtual concat of src (zero outside [0,Tv)).
- * out row-major with leading dimension ldo; accumulate != 0 adds to existing values. */
+ * ldc = ldt = 0 selects the torch weight layout (ldc = taps, ldt = 1); ldc = 1 is the
+ * tap-major layout. accumulate != 0 adds to existing values. */
 typedef struct mst_wgrad_desc {
   int32_t B, M, Tk, Ctot, taps;
   int32_t a, beta, g;
@@ -116,6 +117,7 @@ typedef struct mst_wgrad_desc {
   int32_t accumulate;
   int32_t splitk;            /* 0 = auto */
   int32_t pad1_;
+  int64_t ldc, ldt;          /* output strides per input channel / per tap (0, 0: torch layout) */
 } mst_wgrad_desc;
 
 /* ---- conv/linear GEMMs (MFMA f32) ---- */

@@ -46,7 +46,7 @@ class MstWgradDesc(ctypes.Structure):
                 ("Tv", c_int32), ("P", c_void_p), ("sPb", c_int64), ("sPc", c_int32),
                 ("pad0_", c_int32), ("src", MstSrc * 2), ("out", c_void_p), ("ldo", c_int64),
                 ("scale", c_float), ("accumulate", c_int32), ("splitk", c_int32),
-                ("pad1_", c_int32)]
+                ("pad1_", c_int32), ("ldc", c_int64), ("ldt", c_int64)]
 
 
 P_CONV = ctypes.POINTER(MstConvDesc)

@@ -82,7 +82,9 @@ struct GP {
   unsigned long long seed;
   // wgrad epilogue
   float* out;
-  long long ldo;
+  long long ldo, ldc, ldt;  // column of (c, tap) = c * ldc + tap * ldt
+  int taps, ocustom;
+  float inv_taps;
   float scale;
   int accumulate;
   // split-K slab
@@ -120,7 +122,12 @@ __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
 
 __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) {
   if (m >= p.M || n >= p.N) return;
-  float* o = p.out + (long long)m * p.ldo + n;
+  long long col = n;  // n = c * taps + tap: the column in the torch layout
+  if (p.ocustom) {    // e.g. tap-major weights: column = c * ldc + tap * ldt
+    const int c = (int)(((float)n + 0.5f) * p.inv_taps);  // exact for n < 2^22
+    col = (long long)c * p.ldc + (long long)(n - c * p.taps) * p.ldt;
+  }
+  float* o = p.out + (long long)m * p.ldo + col;
   v *= p.scale;
   if (p.accumulate) v += *o;
   *o = v;
@@ -241,7 +248,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     for (int u = 0; u < 4; ++u) {
       const int m = m0 + km_row + 32 * u;
       const int n = n0 + km_row + 32 * u;
-      const int c = n / TAPS;
+      const int c = n / TAPS;  // N order n = c * taps + tap for every output layout
       const int tap = n - c * TAPS;
       const int abase = m * p.sPc + bdl * (int)p.sPb + t0ref + tlb;
       const int tin0 = p.ta * (t0ref + tlb) + p.tb + p.tg * tap;  // input time at i = 0
@@ -692,6 +699,17 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   p.K = p.nk * BK;
   p.out = out;
   p.ldo = d->ldo;
+  p.taps = d->taps;
+  if (d->ldc == 0 && d->ldt == 0) {
+    p.ldc = d->taps;
+    p.ldt = 1;
+  } else {
+    p.ldc = d->ldc;
+    p.ldt = d->ldt;
+  }
+  p.ocustom = !(p.ldc == d->taps && p.ldt == 1);
+  p.inv_taps = 1.0f / (float)d->taps;
+  MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
   p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
@@ -704,7 +722,8 @@ int wgrad_sources(const mst_wgrad_desc* d, mst_src* srcs, float** outs) {
   outs[0] = d->out;
   if (d->src[1].C <= 0) return 1;
   srcs[1] = d->src[1];
-  outs[1] = d->out + (long long)d->src[0].C * d->taps;
+  const long long ldc = d->ldc == 0 && d->ldt == 0 ? d->taps : d->ldc;
+  outs[1] = d->out + (long long)d->src[0].C * ldc;
   return 2;
 }
 

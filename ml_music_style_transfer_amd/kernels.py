@@ -121,7 +121,10 @@ def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt
            2.0 * M * B * Tn * d.Ctot * taps, "conv", (M, B * Tn, d.Ctot * taps, taps, a, nb))
 
 
-def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate=False, splitk=0):
+def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, ldc=0, ldt=0, scale=1.0, accumulate=False,
+               splitk=0):
+    """out[m*ldo + c*ldc + tap*ldt] (+)= scale * sum_{b,t} P[b][m][t] X(b, c, a*t+beta+g*tap);
+    ldc = ldt = 0 means the torch layout (ldc = taps, ldt = 1)."""
     lib = _lib()
     d = L.MstWgradDesc()
     B, M, Tk = P.shape
@@ -135,6 +138,7 @@ def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate
     d.src[1] = _src(srcs[1] if len(srcs) > 1 else None)
     d.out = out.data_ptr()
     d.ldo = ldo
+    d.ldc, d.ldt = ldc, ldt
     d.scale = scale
     d.accumulate = 1 if accumulate else 0
     d.splitk = splitk
@@ -145,25 +149,31 @@ def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, scale=1.0, accumulate
            (M, d.Ctot * taps, B * Tk, taps, a, nb))
 
 
+def _wgrad_out(dW):
+    """(ldo, ldc, ldt) of a (d0, C, taps) weight-gradient tensor in any layout."""
+    return dW.stride(0), dW.stride(1), dW.stride(2)
+
+
 # ---------------------------------------------------------------- Conv1d k3 p1
+# Weights may be in the torch layout or tap-major (model.slot_view): every A operand takes
+# its strides from the tensor.
 def conv3_fwd(srcs, W, bias, out, act=L.ACT_NONE):
     B, Cout, T = out.shape
-    Cin = W.shape[1]
-    conv_like(B=B, M=Cout, Tn=T, srcs=srcs, Tv=T, taps=3, a=1, beta=-1, g=1, A=W, sAm=Cin * 3,
-              sAc=3, sAt=1, dsts=[(out, 0, None, 1.0)], bias=bias, act=act)
+    conv_like(B=B, M=Cout, Tn=T, srcs=srcs, Tv=T, taps=3, a=1, beta=-1, g=1, A=W, sAm=W.stride(0),
+              sAc=W.stride(1), sAt=W.stride(2), dsts=[(out, 0, None, 1.0)], bias=bias, act=act)
 
 
 def conv3_dgrad(dY, W, dsts):
     B, Cout, T = dY.shape
     Cin = W.shape[1]
-    conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=3, a=1, beta=1, g=-1, A=W, sAm=3,
-              sAc=Cin * 3, sAt=1, dsts=dsts)
+    conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=3, a=1, beta=1, g=-1, A=W,
+              sAm=W.stride(1), sAc=W.stride(0), sAt=W.stride(2), dsts=dsts)
 
 
 def conv3_wgrad(dY, srcs, dW, accumulate):
-    Cin = dW.shape[1]
-    wgrad_like(P=dY, srcs=srcs, Tv=dY.shape[2], taps=3, a=1, beta=-1, g=1, out=dW, ldo=Cin * 3,
-               accumulate=accumulate)
+    ldo, ldc, ldt = _wgrad_out(dW)
+    wgrad_like(P=dY, srcs=srcs, Tv=dY.shape[2], taps=3, a=1, beta=-1, g=1, out=dW, ldo=ldo, ldc=ldc,
+               ldt=ldt, accumulate=accumulate)
 
 
 # ------------------------------------------------- ConvTranspose1d(k, s=2, p=1)
@@ -181,8 +191,8 @@ def convT2_fwd(x, W, bias, out):
         if nq == 0 or Tn <= 0:
             continue
         conv_like(B=B, M=Cout, Tn=Tn, srcs=[(x, 0)], Tv=Tin, taps=nq, a=1, beta=p, g=-1, A=W,
-                  A_off=1 - p, sAm=k, sAc=Cout * k, sAt=2, dsts=[(out, 0, None, 1.0)], ostride=2,
-                  ophase=p, bias=bias)
+                  A_off=(1 - p) * W.stride(2), sAm=W.stride(1), sAc=W.stride(0), sAt=2 * W.stride(2),
+                  dsts=[(out, 0, None, 1.0)], ostride=2, ophase=p, bias=bias)
 
 
 def convT2_dgrad(dY, W, dsts):
@@ -190,34 +200,37 @@ def convT2_dgrad(dY, W, dsts):
     B, _, Tout = dY.shape
     Tin = dsts[0][0].shape[2]
     conv_like(B=B, M=Cin, Tn=Tin, srcs=[(dY, 0)], Tv=Tout, taps=k, a=2, beta=-1, g=1, A=W,
-              sAm=Cout * k, sAc=k, sAt=1, dsts=dsts)
+              sAm=W.stride(0), sAc=W.stride(1), sAt=W.stride(2), dsts=dsts)
 
 
 def convT2_wgrad(x, dY, dW, accumulate):
     Cin, Cout, k = dW.shape
-    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=k, a=2, beta=-1, g=1, out=dW,
-               ldo=Cout * k, accumulate=accumulate)
+    ldo, ldc, ldt = _wgrad_out(dW)
+    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=k, a=2, beta=-1, g=1, out=dW, ldo=ldo,
+               ldc=ldc, ldt=ldt, accumulate=accumulate)
 
 
 # ------------------------------------------- ConvTranspose1d(k=3, s=1, p=1) (lastconv)
 def convT1_fwd(x, W, bias, out, alpha=1.0, act=L.ACT_NONE):
     Cin, Cout, k = W.shape
     B, _, T = x.shape
-    conv_like(B=B, M=Cout, Tn=T, srcs=[(x, 0)], Tv=T, taps=k, a=1, beta=1, g=-1, A=W, sAm=k,
-              sAc=Cout * k, sAt=1, dsts=[(out, 0, None, 1.0)], alpha=alpha, bias=bias, act=act)
+    conv_like(B=B, M=Cout, Tn=T, srcs=[(x, 0)], Tv=T, taps=k, a=1, beta=1, g=-1, A=W,
+              sAm=W.stride(1), sAc=W.stride(0), sAt=W.stride(2), dsts=[(out, 0, None, 1.0)],
+              alpha=alpha, bias=bias, act=act)
 
 
 def convT1_dgrad(dY, W, dx, alpha=1.0):
     Cin, Cout, k = W.shape
     B, _, T = dY.shape
     conv_like(B=B, M=Cin, Tn=T, srcs=[(dY, 0)], Tv=T, taps=k, a=1, beta=-1, g=1, A=W,
-              sAm=Cout * k, sAc=k, sAt=1, dsts=[(dx, 0, None, 1.0)], alpha=alpha)
+              sAm=W.stride(0), sAc=W.stride(1), sAt=W.stride(2), dsts=[(dx, 0, None, 1.0)],
+              alpha=alpha)
 
 
 def convT1_wgrad(x, dY, dW, accumulate, scale=1.0):
-    Cin, Cout, k = dW.shape
-    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=k, a=1, beta=-1, g=1, out=dW,
-               ldo=Cout * k, scale=scale, accumulate=accumulate)
+    ldo, ldc, ldt = _wgrad_out(dW)
+    wgrad_like(P=x, srcs=[(dY, 0)], Tv=dY.shape[2], taps=dW.shape[2], a=1, beta=-1, g=1, out=dW,
+               ldo=ldo, ldc=ldc, ldt=ldt, scale=scale, accumulate=accumulate)
 
 
 # ------------------------------------------------------- Linear over NCL channels

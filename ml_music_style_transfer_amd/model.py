@@ -35,6 +35,17 @@ def upconv1x2(in_channels, out_channels, kernel):
     return nn.ConvTranspose1d(in_channels, out_channels, kernel_size=kernel, stride=2, padding=1)
 
 
+def slot_view(buf, p):
+    """View of a flat-buffer slot with p's shape. 3-D conv weights (Conv1d (Cout, Cin, k),
+    ConvTranspose1d (Cin, Cout, k)) are stored tap-major, i.e. as (d0, k, d1) permuted back
+    to (d0, d1, k): the GEMM loaders then read channel-contiguous rows (float4 along K for
+    the forward of Conv1d, along M for its input gradient)."""
+    if p.dim() == 3:
+        d0, d1, k = p.shape
+        return buf.view(d0, k, d1).permute(0, 2, 1)
+    return buf.view_as(p)
+
+
 def _require_cuda(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
@@ -353,10 +364,11 @@ class PerformanceNet(nn.Module):
         grad = torch.zeros(off, device=dev, dtype=torch.float32)
         with torch.no_grad():
             for p, o in zip(params, offsets):
-                flat[o:o + p.numel()].copy_(p.data.reshape(-1))
-                p.data = flat[o:o + p.numel()].view_as(p)
+                dst = slot_view(flat[o:o + p.numel()], p)
+                dst.copy_(p.data)
+                p.data = dst
                 if p.grad is not None:
-                    g = grad[o:o + p.numel()].view_as(p)
+                    g = slot_view(grad[o:o + p.numel()], p)
                     g.copy_(p.grad)
                     p.grad = g
         me = weakref.ref(self)
@@ -381,7 +393,7 @@ class PerformanceNet(nn.Module):
             if ent is None:
                 return None
             o, n = ent
-            return f["grad"][o:o + n].view_as(p)
+            return slot_view(f["grad"][o:o + n], p)
         return E.GradSink(flat_grad_of, on_ready)
 
     def _apply(self, fn, *args, **kwargs):

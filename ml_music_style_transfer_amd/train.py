@@ -23,7 +23,7 @@ import torch
 from . import dp
 from . import engine as E
 from . import kernels as K
-from .model import PerformanceNet
+from .model import PerformanceNet, slot_view
 
 
 class hyperparams(object):
@@ -111,8 +111,8 @@ class Adam(torch.optim.Optimizer):
                     index = self._owner._flat["index"]
                     for p in params:
                         o, k = index[id(p)]
-                        self.state[p] = {"step": None, "exp_avg": m[o:o + k].view_as(p),
-                                         "exp_avg_sq": v[o:o + k].view_as(p)}
+                        self.state[p] = {"step": None, "exp_avg": slot_view(m[o:o + k], p),
+                                         "exp_avg_sq": slot_view(v[o:o + k], p)}
                 st["step"] += 1
                 t = st["step"]
                 bc1 = 1 - b1 ** t

@@ -74,6 +74,81 @@ def test_conv3_wgrad_time_classes(cuda, B, T, splitk):
     _close(dW, Wr.grad, B * T, what=f"wgrad B={B} T={T}")
 
 
+def _tap_major(t, cuda):
+    """A (d0, d1, k) weight stored tap-major, as model.slot_view lays out flat-buffer slots."""
+    d0, d1, k = t.shape
+    out = torch.empty(d0, k, d1, device=cuda).permute(0, 2, 1)
+    out.copy_(t)
+    return out
+
+
+@pytest.mark.parametrize("B,T", [(2, 37), (32, 15)])
+def test_conv3_tap_major_weights(cuda, B, T):
+    """Tap-major weights (channel-contiguous A rows) and tap-major weight gradients, with a
+    two-source virtual concat and split dgrad destinations."""
+    from ml_music_style_transfer_amd import kernels as K
+    C1, C2, Cout = 36, 20, 44
+    u, r = _r(B, C1, T, seed=41), _r(B, C2, T + 1, seed=42)
+    W, b = _r(Cout, C1 + C2, 3, seed=43), _r(Cout, seed=44)
+    c = (T + 1 - T) // 2
+    rc = torch.zeros(B, C2, T, dtype=torch.float64)
+    rc[:, :, :] = r[:, :, c:c + T]
+    ur, rcr = u.clone().requires_grad_(True), rc.clone().requires_grad_(True)
+    Wr = W.clone().requires_grad_(True)
+    yr = _conv1d_ref(torch.cat([ur, rcr], 1), Wr, b)
+    dy = _r(B, Cout, T, seed=45)
+    yr.backward(dy)
+    ud, rd, bd, dyd = u.float().to(cuda), r.float().to(cuda), b.float().to(cuda), dy.float().to(cuda)
+    Wd = _tap_major(W.float(), cuda)
+    y = torch.empty(B, Cout, T, device=cuda)
+    K.conv3_fwd([(ud, 0), (rd, c)], Wd, bd, y)
+    _close(y, yr.detach(), (C1 + C2) * 3, what="tap-major fwd")
+    du, dr = torch.empty_like(ud), torch.zeros_like(rd)
+    K.conv3_dgrad(dyd, Wd, [(du, 0, None, 1.0), (dr, c, None, 1.0)])
+    _close(du, ur.grad, Cout * 3, what="tap-major dgrad")
+    _close(dr[:, :, c:c + T], rcr.grad, Cout * 3, what="tap-major dgrad skip")
+    dW = _tap_major(torch.full((Cout, C1 + C2, 3), float("nan")), cuda)
+    K.conv3_wgrad(dyd, [(ud, 0), (rd, c)], dW, False)
+    _close(dW, Wr.grad, B * T, what="tap-major wgrad")
+    K.conv3_wgrad(dyd, [(ud, 0), (rd, c)], dW, True)
+    _close(dW, 2 * Wr.grad, 2 * B * T, what="tap-major wgrad acc")
+
+
+@pytest.mark.parametrize("k", [2, 3, 4, 6])
+def test_convT_tap_major_weights(cuda, k):
+    from ml_music_style_transfer_amd import kernels as K
+    B, Cin, Cout, Tin = 3, 40, 36, 15
+    x, W, b = _r(B, Cin, Tin, seed=46), _r(Cin, Cout, k, seed=47), _r(Cout, seed=48)
+    xr, Wr = x.clone().requires_grad_(True), W.clone().requires_grad_(True)
+    yr = F.conv_transpose1d(xr, Wr, b, stride=2, padding=1)
+    dy = _r(*yr.shape, seed=49)
+    yr.backward(dy)
+    xd, bd, dyd = x.float().to(cuda), b.float().to(cuda), dy.float().to(cuda)
+    Wd = _tap_major(W.float(), cuda)
+    y = torch.empty(*yr.shape, device=cuda)
+    K.convT2_fwd(xd, Wd, bd, y)
+    _close(y, yr.detach(), Cin * k, what="tap-major convT fwd")
+    dx = torch.empty_like(xd)
+    K.convT2_dgrad(dyd, Wd, [(dx, 0, None, 1.0)])
+    _close(dx, xr.grad, Cout * k, what="tap-major convT dgrad")
+    dW = _tap_major(torch.full((Cin, Cout, k), float("nan")), cuda)
+    K.convT2_wgrad(xd, dyd, dW, False)
+    _close(dW, Wr.grad, B * Tin, what="tap-major convT wgrad")
+    if k == 3:  # lastconv geometry (stride 1)
+        xr2, Wr2 = x.clone().requires_grad_(True), W.clone().requires_grad_(True)
+        yr2 = F.conv_transpose1d(xr2, Wr2, b, stride=1, padding=1)
+        dy2 = _r(*yr2.shape, seed=50)
+        yr2.backward(dy2)
+        y2 = torch.empty(*yr2.shape, device=cuda)
+        K.convT1_fwd(xd, Wd, bd, y2)
+        _close(y2, yr2.detach(), Cin * k, what="tap-major convT1 fwd")
+        dx2 = torch.empty_like(xd)
+        K.convT1_dgrad(dy2.float().to(cuda), Wd, dx2)
+        _close(dx2, xr2.grad, Cout * k, what="tap-major convT1 dgrad")
+        K.convT1_wgrad(xd, dy2.float().to(cuda), dW, False)
+        _close(dW, Wr2.grad, B * Tin, what="tap-major convT1 wgrad")
+
+
 @pytest.mark.parametrize("splitk", [2, 5])
 def test_gemm_splitk(cuda, splitk):
     from ml_music_style_transfer_amd import kernels as K
