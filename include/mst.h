@@ -132,14 +132,19 @@ int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* workspace, size_t ws_byte
 int mst_instnorm_lrelu_fwd_f32(const float* y, int64_t rows, int32_t T, float eps, float slope,
                                float* a, float* pooled, float* mean, float* rstd, void* stream);
 /* dy = d/dy of the forward, given upstream grads of a (d_a, nullable) and of pooled
- * (d_pool0, d_pool1: nullable, summed). Recomputes z and the pool argmax from y. */
+ * (d_pool0, d_pool1: nullable, summed). Recomputes z and the pool argmax from y.
+ * rowsum (nullable, length rows): the sum over t of each written dy row, i.e. the producing
+ * layer's bias gradient per (b, c) (reduce over b with mst_bias_grad_rows_f32). */
 int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* rstd, int64_t rows,
                                int32_t T, float slope, const float* d_a, const float* d_pool0,
-                               const float* d_pool1, float* dy, void* stream);
+                               const float* d_pool1, float* dy, float* rowsum, void* stream);
 
 /* db[c] (+)= sum_{b,t} dy[b][c][t] for an NCL tensor (B, C, T). */
 int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float scale, float* db,
                       int32_t accumulate, void* stream);
+/* db[c] (+)= scale * sum_b rowsum[b*C + c] (row sums from mst_instnorm_lrelu_bwd_f32). */
+int mst_bias_grad_rows_f32(const float* rowsum, int32_t B, int32_t C, float scale, float* db,
+                           int32_t accumulate, void* stream);
 
 /* ---- lastconv LeakyReLU + L1 loss (model.py:299, train.py:132-135) ----
  * fwd: y = lrelu(ypre) written to y (nullable); loss_partials[nblocks] (double) then

@@ -9,7 +9,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmst_hip.so")
+# MST_LIB_PATH: alternative build of the same library (kernel A/B experiments; dev only)
+LIB_PATH = os.environ.get("MST_LIB_PATH") or os.path.join(_HERE, "libmst_hip.so")
 
 c_void_p, c_int32, c_int64, c_float, c_uint64, c_size_t = (
     ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64, ctypes.c_size_t)
@@ -61,7 +62,9 @@ SIGNATURES = {
     "mst_instnorm_lrelu_fwd_f32": (c_int32, [c_void_p, c_int64, c_int32, c_float, c_float, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_void_p]),
     "mst_instnorm_lrelu_bwd_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_float,
-                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                             c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mst_bias_grad_rows_f32": (c_int32, [c_void_p, c_int32, c_int32, c_float, c_void_p, c_int32,
+                                         c_void_p]),
     "mst_bias_grad_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
                                     c_void_p]),
     "mst_l1_workspace_size": (c_size_t, [c_int64]),

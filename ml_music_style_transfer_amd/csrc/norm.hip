@@ -111,7 +111,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
                                                      const float* __restrict__ d_a,
                                                      const float* __restrict__ dp0,
                                                      const float* __restrict__ dp1,
-                                                     float* __restrict__ dy) {
+                                                     float* __restrict__ dy,
+                                                     float* __restrict__ rowsum) {
   const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -147,11 +148,24 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
   s1 = wave_sum(s1) / (float)T;
   s2 = wave_sum(s2) / (float)T;
   float* dr = dy + row * T;
+  float rs = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     int i0 = 2 * lane + 128 * q;
-    if (i0 < T) dr[i0] = r * (g0[q] - s1 - z0[q] * s2);
-    if (i0 + 1 < T) dr[i0 + 1] = r * (g1[q] - s1 - z1[q] * s2);
+    if (i0 < T) {
+      const float v = r * (g0[q] - s1 - z0[q] * s2);
+      dr[i0] = v;
+      rs += v;
+    }
+    if (i0 + 1 < T) {
+      const float v = r * (g1[q] - s1 - z1[q] * s2);
+      dr[i0 + 1] = v;
+      rs += v;
+    }
+  }
+  if (rowsum) {
+    rs = wave_sum(rs);
+    if (lane == 0) rowsum[row] = rs;
   }
 }
 
@@ -180,7 +194,8 @@ __global__ __launch_bounds__(256) void in_bwd_long_kernel(const float* __restric
                                                           const float* __restrict__ d_a,
                                                           const float* __restrict__ dp0,
                                                           const float* __restrict__ dp1,
-                                                          float* __restrict__ dy) {
+                                                          float* __restrict__ dy,
+                                                          float* __restrict__ rowsum) {
   const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= rows) return;
@@ -199,11 +214,30 @@ __global__ __launch_bounds__(256) void in_bwd_long_kernel(const float* __restric
   }
   s1 = wave_sum(s1) / (float)T;
   s2 = wave_sum(s2) / (float)T;
+  float rs = 0.f;
   for (int i = lane; i < T; i += 64) {
     float z;
     float g = in_bwd_g(yr, i, T, Tp, mu, r, slope, dar, p0, p1, &z);
-    dy[row * T + i] = r * (g - s1 - z * s2);
+    const float v = r * (g - s1 - z * s2);
+    dy[row * T + i] = v;
+    rs += v;
   }
+  if (rowsum) {
+    rs = wave_sum(rs);
+    if (lane == 0) rowsum[row] = rs;
+  }
+}
+
+// db[c] = scale * sum_b rowsum[b * C + c] (+ db[c]): the bias gradient from per-row sums.
+__global__ __launch_bounds__(256) void bias_rows_kernel(const float* __restrict__ rowsum, int B,
+                                                        int C, float scale, float* __restrict__ db,
+                                                        int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += rowsum[(long long)b * C + c];
+  s *= scale;
+  db[c] = accumulate ? db[c] + s : s;
 }
 
 // db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one block per channel.
@@ -408,16 +442,16 @@ int mst_instnorm_lrelu_fwd_f32(const float* y, int64_t rows, int32_t T, float ep
 
 int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* rstd, int64_t rows,
                                int32_t T, float slope, const float* d_a, const float* d_pool0,
-                               const float* d_pool1, float* dy, void* stream) {
+                               const float* d_pool1, float* dy, float* rowsum, void* stream) {
   MST_REQUIRE(y && mean && rstd && dy && rows > 0 && T > 1);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
-  if (np <= 1) hipLaunchKernelGGL(in_bwd_kernel<1>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
-  else if (np <= 2) hipLaunchKernelGGL(in_bwd_kernel<2>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
-  else if (np <= 4) hipLaunchKernelGGL(in_bwd_kernel<4>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
-  else if (np <= 8) hipLaunchKernelGGL(in_bwd_kernel<8>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
-  else hipLaunchKernelGGL(in_bwd_long_kernel, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy);
+  if (np <= 1) hipLaunchKernelGGL(in_bwd_kernel<1>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
+  else if (np <= 2) hipLaunchKernelGGL(in_bwd_kernel<2>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
+  else if (np <= 4) hipLaunchKernelGGL(in_bwd_kernel<4>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
+  else if (np <= 8) hipLaunchKernelGGL(in_bwd_kernel<8>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
+  else hipLaunchKernelGGL(in_bwd_long_kernel, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
@@ -427,6 +461,15 @@ int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float sc
   MST_REQUIRE(dy && db && B > 0 && C > 0 && T > 0);
   hipLaunchKernelGGL(bias_grad_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, B, C, T,
                      scale, db, accumulate);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_bias_grad_rows_f32(const float* rowsum, int32_t B, int32_t C, float scale, float* db,
+                           int32_t accumulate, void* stream) {
+  MST_REQUIRE(rowsum && db && B > 0 && C > 0);
+  hipLaunchKernelGGL(bias_rows_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     rowsum, B, C, scale, db, accumulate);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }

@@ -13,7 +13,9 @@ possible:
     loaders read two sources with time offsets, and dgrad epilogues split the
     concatenated input gradient back into its parts;
   * the maxpool gradient and the skip gradient of an encoder level are summed
-    inside the InstanceNorm backward kernel (no accumulation pass);
+    inside the InstanceNorm backward kernel (no accumulation pass), which also emits the
+    per-(b, c) row sums of its output: the producing conv's bias gradient needs only a
+    (B, C) reduction instead of another pass over dy;
   * MBRBlock x4 returns 16*x exactly (model.py:172 discards its residual sum),
     so its dead convolutions are skipped and the 16 folds into lastconv's GEMM
     (alpha) — output- and gradient-identical to the reference;
@@ -82,20 +84,20 @@ def downconv_fwd(W1, b1, W2, b2, x, pool):
 def downconv_bwd(params, saved, sink, d_before=None, d_pool0=None, d_pool1=None, need_dx=True):
     W1, b1, W2, b2 = params
     x, y1, m1, r1, a1, y2, m2, r2 = saved
-    dy2 = K.in_lrelu_bwd(y2, m2, r2, d_before, d_pool0, d_pool1)
+    dy2, rs2 = K.in_lrelu_bwd(y2, m2, r2, d_before, d_pool0, d_pool1, rowsum=True)
     g, acc = sink.target(W2)
     K.conv3_wgrad(dy2, [(a1, 0)], g, acc)
     g, acc = sink.target(b2)
-    K.bias_grad(dy2, g, acc)
+    K.bias_grad_rows(rs2, g, acc)
     da1 = torch.empty_like(a1)
     K.conv3_dgrad(dy2, W2, [(da1, 0, None, 1.0)])
     del dy2
-    dy1 = K.in_lrelu_bwd(y1, m1, r1, da1)
+    dy1, rs1 = K.in_lrelu_bwd(y1, m1, r1, da1, rowsum=True)
     del da1
     g, acc = sink.target(W1)
     K.conv3_wgrad(dy1, [(x, 0)], g, acc)
     g, acc = sink.target(b1)
-    K.bias_grad(dy1, g, acc)
+    K.bias_grad_rows(rs1, g, acc)
     if not need_dx:
         return None
     dx = torch.empty_like(x)
@@ -185,12 +187,12 @@ def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_
     Wu, bu, W1, b1, W2, b2 = params
     (dec, u_pre, mu_, ru_, u, res, c_res, v_pre, mv_, rv_, v, cond, c_cond, w_pre, mw_,
      rw_) = saved
-    dw_pre = K.in_lrelu_bwd(w_pre, mw_, rw_, d_w)
+    dw_pre, rs_w = K.in_lrelu_bwd(w_pre, mw_, rw_, d_w, rowsum=True)
     srcs2 = [(v, 0)] + ([(cond, c_cond)] if cond is not None else [])
     g, acc = sink.target(W2)
     K.conv3_wgrad(dw_pre, srcs2, g, acc)
     g, acc = sink.target(b2)
-    K.bias_grad(dw_pre, g, acc)
+    K.bias_grad_rows(rs_w, g, acc)
     dv = torch.empty_like(v)
     dsts = [(dv, 0, None, 1.0)]
     d_cond = None
@@ -199,22 +201,22 @@ def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_
         dsts.append((d_cond, c_cond, None, 1.0))
     K.conv3_dgrad(dw_pre, W2, dsts)
     del dw_pre
-    dv_pre = K.in_lrelu_bwd(v_pre, mv_, rv_, dv)
+    dv_pre, rs_v = K.in_lrelu_bwd(v_pre, mv_, rv_, dv, rowsum=True)
     del dv
     g, acc = sink.target(W1)
     K.conv3_wgrad(dv_pre, [(u, 0), (res, c_res)], g, acc)
     g, acc = sink.target(b1)
-    K.bias_grad(dv_pre, g, acc)
+    K.bias_grad_rows(rs_v, g, acc)
     du = torch.empty_like(u)
     d_res = _grad_buffer_for_bypass(res, c_res, u.shape[2])
     K.conv3_dgrad(dv_pre, W1, [(du, 0, None, 1.0), (d_res, c_res, res_gate, res_gate_scale)])
     del dv_pre
-    du_pre = K.in_lrelu_bwd(u_pre, mu_, ru_, du)
+    du_pre, rs_u = K.in_lrelu_bwd(u_pre, mu_, ru_, du, rowsum=True)
     del du
     g, acc = sink.target(Wu)
     K.convT2_wgrad(dec, du_pre, g, acc)
     g, acc = sink.target(bu)
-    K.bias_grad(du_pre, g, acc)
+    K.bias_grad_rows(rs_u, g, acc)
     d_dec = torch.empty_like(dec)
     K.convT2_dgrad(du_pre, Wu, [(d_dec, 0, dec_gate, dec_gate_scale)])
     return d_res, d_dec, d_cond

@@ -266,13 +266,23 @@ def in_lrelu_fwd(y, pool):
     return a, pooled, mean, rstd
 
 
-def in_lrelu_bwd(y, mean, rstd, d_a=None, d_pool0=None, d_pool1=None):
+def in_lrelu_bwd(y, mean, rstd, d_a=None, d_pool0=None, d_pool1=None, rowsum=False):
+    """IN + LeakyReLU (+ maxpool) backward. rowsum=True also returns the (B, C) per-row sums of
+    dy (the producing conv's bias gradient before the batch reduction, bias_grad_rows)."""
     B, C, T = y.shape
     dy = torch.empty_like(y)
+    rs = empty(B, C, like=y) if rowsum else None
     L.check(_lib().mst_instnorm_lrelu_bwd_f32(L.ptr(y), L.ptr(mean), L.ptr(rstd), B * C, T, SLOPE,
                                               L.ptr(d_a), L.ptr(d_pool0), L.ptr(d_pool1), L.ptr(dy),
-                                              L.stream()), "instnorm_bwd")
-    return dy
+                                              L.ptr(rs), L.stream()), "instnorm_bwd")
+    return (dy, rs) if rowsum else dy
+
+
+def bias_grad_rows(rs, db, accumulate):
+    """db (+)= sum over the batch of per-(b, c) row sums (from in_lrelu_bwd(rowsum=True))."""
+    B, C = rs.shape
+    L.check(_lib().mst_bias_grad_rows_f32(L.ptr(rs), B, C, 1.0, L.ptr(db), 1 if accumulate else 0,
+                                          L.stream()), "bias_grad_rows")
 
 
 def bias_grad(dy, db, accumulate):

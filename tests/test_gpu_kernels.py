@@ -299,9 +299,17 @@ def test_instnorm_lrelu_pool(cuda, T, pool):
     _close(ad, a.detach(), 10, rtol=1e-5, what="IN fwd")
     if pool:
         _close(pd, outs[1].detach(), 10, rtol=1e-5, what="pool fwd")
-    dy = K.in_lrelu_bwd(yd, mean, rstd, da.float().to(cuda), dp.float().to(cuda) if pool else None,
-                        dp2.float().to(cuda) if pool else None)
+    dy, rs = K.in_lrelu_bwd(yd, mean, rstd, da.float().to(cuda), dp.float().to(cuda) if pool else None,
+                            dp2.float().to(cuda) if pool else None, rowsum=True)
     _close(dy, yr.grad, 10, rtol=2e-5, what="IN bwd")
+    # fused row sums == sum over t of the written dy rows; bias gradient from them
+    _close(rs, dy.double().sum(2).cpu(), T, rtol=1e-6, what="IN bwd row sums")
+    db, db2 = torch.empty(C, device=cuda), torch.empty(C, device=cuda)
+    K.bias_grad_rows(rs, db, False)
+    K.bias_grad(dy, db2, False)
+    _close(db, db2.double().cpu(), B * T, rtol=1e-6, what="bias from row sums")
+    K.bias_grad_rows(rs, db, True)
+    _close(db, 2 * db2.double().cpu(), 2 * B * T, rtol=1e-6, what="bias from row sums acc")
 
 
 def test_l1_mse_adam(cuda):
