@@ -36,7 +36,6 @@ constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256, LDK = BK + 4;
 constexpr uint32_t OOB = 0x7FFFFFF0u;  // byte offset past every descriptor's num_records
 constexpr int MAXCLS = 8;              // wgrad K classes
 
-
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
 struct GP {
@@ -172,9 +171,8 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear id % 8),
-  // each with its own L2. Renumber so every XCD runs one contiguous range of tiles, N fastest:
-  // the workgroups that share an A panel (one M tile, all N tiles) then sit on one XCD and
-  // read it through one L2 instead of eight.
+  // each with its own L2. Renumber so every XCD runs one contiguous range of tiles: the
+  // workgroups that share A and B panels then sit on one XCD and read them through one L2.
   int n_t, m_t, split;
   {
     const int nx = gridDim.x, ny = gridDim.y;
@@ -182,9 +180,18 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     const int w = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
     const int q = W >> 3, r = W & 7, xcd = w & 7;
     const int t = xcd * q + min(xcd, r) + (w >> 3);
-    n_t = t % nx;
-    m_t = (t / nx) % ny;
+    // grouped order inside a split: runs of GM M-tiles x all N-tiles, M fastest within a run,
+    // so an XCD's contiguous range is a near-square block of tiles (8 x 8 when it holds 64)
+    // and both its A and its B panels are re-read from the XCD's L2
     split = t / (nx * ny);
+    const int t2 = t - split * nx * ny;
+    const int GM = ny < 8 ? ny : 8;
+    const int grp = t2 / (GM * nx);
+    const int fm = grp * GM;
+    const int gm = ny - fm < GM ? ny - fm : GM;
+    const int tg = t2 - grp * GM * nx;
+    m_t = fm + tg % gm;
+    n_t = tg / gm;
   }
   const int n0 = n_t * BN;
   const int m0 = m_t * BM;
