@@ -416,31 +416,65 @@ __device__ __forceinline__ c2 gl_bin(const float2* cur, const float2* prev, cons
   return a;
 }
 
-__global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict__ cur,
+// floor(x / d) for 0 <= x < 2^24 via a float reciprocal and one correction step.
+__device__ __forceinline__ int div_hop(int x, int d, float inv) {
+  int q = (int)((float)x * inv);
+  const int r = x - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
+}
+
+// OLA per round: every thread owns 16 output samples sp = plo + tid + 512 i (padded
+// coordinates); frame f covers sp when 0 <= sp - f*hop < NFFT. Each wave leaves its frame's
+// windowed, 1/NC-scaled samples in its scratch, and every thread adds, for each of its samples,
+// only the frames of this round that cover it (in increasing frame order). The
+// window-sum-square of interior samples depends on sp mod hop only (table wssr, built once
+// per workgroup in the same summation order); samples near the clip ends sum it directly.
+__global__ __launch_bounds__(512, 2) void istft_kernel(const float2* __restrict__ cur,
                                                        const float2* __restrict__ prev,
                                                        const float* __restrict__ mag, float beta,
                                                        int normalize, int T, int hop,
                                                        float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) c2 scratch[WAVES * SCR];
   __shared__ c2 qt[QT];
+  __shared__ c2 eht[64];
+  __shared__ float wssr[512];
   const int b = blockIdx.y;
   const int L = hop * (T - 1);
   const int s0 = blockIdx.x * ISEG;  // segment start (unpadded coords)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   build_qtable(qt);
+  if (threadIdx.x < 64) {
+    double sn, cs;
+    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
+    eht[threadIdx.x] = mk((float)cs, (float)-sn);
+  }
   __syncthreads();
+  const int K = NFFT / hop;  // frames covering an interior sample (when hop divides NFFT)
+  const bool table = (NFFT % hop) == 0 && hop <= 512;
+  if (table) {
+    for (int r = threadIdx.x; r < hop; r += blockDim.x) {
+      float s = 0.f;
+      for (int k = K - 1; k >= 0; --k) {  // frames in increasing order: m decreasing
+        const float w = hann_w(qt, r + hop * k);
+        s += w * w;
+      }
+      wssr[r] = s;
+    }
+  }
   c2* S = scratch + wave * SCR;
-  // frames overlapping padded range [s0 + 1024, s0 + 1024 + ISEG)
-  const int plo = s0 + NFFT / 2, phi = s0 + NFFT / 2 + ISEG;  // [plo, phi)
+  const int plo = s0 + NFFT / 2, phi = s0 + NFFT / 2 + ISEG;  // padded range [plo, phi)
   int flo = (plo - NFFT) >= 0 ? (plo - NFFT) / hop + 1 : 0;
-  if (flo < 0) flo = 0;
   int fhi = (phi - 1) / hop;  // frame f starts at f*hop < phi
   if (fhi > T - 1) fhi = T - 1;
-  float acc[16], wss[16];
+  float acc[16];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = wss[i] = 0.f;
+  for (int i = 0; i < 16; ++i) acc[i] = 0.f;
   const bool norm = normalize != 0;
   const c2 e1 = tw<false>(qt, lane);  // W2048^lane
+  const float scale = 1.f / NC;
+  const float inv_hop = 1.f / (float)hop;
   for (int fb = flo; fb <= fhi; fb += WAVES) {
     const int f = fb + wave;
     if (f <= fhi) {
@@ -459,24 +493,34 @@ __global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict_
         c2 xe = (Xk + Xc) * 0.5f;
         c2 xo = cmul(Xk - Xc, conj(tw_bin(e1, j))) * 0.5f;
         v[j] = xe + mk(-xo.y, xo.x);  // Xe + i Xo
+        // bound the loads in flight (5 floats per bin) so the frame fits 128 VGPRs
+        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
       fft1024<true>(v, S, qt, lane);
+      // window (sin^2 form, as the STFT) and 1/NC, in place: S[n] = (x[2n], x[2n+1])
+      const c2 eh = eht[lane];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int n = lane + 64 * j;
+        const c2 z = S[n];
+        S[n] = mk(z.x * (hann_sq(e1, j) * scale), z.y * (hann_sq(eh, j) * scale));
+      }
     }
     __syncthreads();
-    // accumulate frames fb .. fb+7 into own samples
-    const int nf = min(WAVES, fhi - fb + 1);
-    for (int w = 0; w < nf; ++w) {
-      const int f = fb + w;
-      const float* fr = reinterpret_cast<const float*>(scratch + w * SCR);
+    const int fe = min(fb + WAVES - 1, fhi);
+    // An opaque zero keeps the per-sample values below from being hoisted out of the frame
+    // loop (16 of them live across the FFT would not fit 128 VGPRs).
+    int zero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int sp = s0 + NFFT / 2 + threadIdx.x + 512 * i;
-        const int m = sp - f * hop;
-        if (m >= 0 && m < NFFT) {
-          float wv = hann_w(qt, m);
-          acc[i] += wv * (fr[m] * (1.f / NC));
-          wss[i] += wv * wv;
-        }
+    for (int i = 0; i < 16; ++i) {
+      const int sp = plo + threadIdx.x + 512 * i + zero;
+      const int q = div_hop(sp, hop, inv_hop);     // last frame covering sp
+      const int f_first = max(fb, q - (NFFT - 1) / hop);
+      const int f_last = min(fe, q);
+      for (int fr = f_first; fr <= f_last; ++fr) {
+        const int m = sp - fr * hop;
+        if (m < NFFT) acc[i] += reinterpret_cast<const float*>(scratch + (fr - fb) * SCR)[m];
       }
     }
     __syncthreads();
@@ -485,7 +529,21 @@ __global__ __launch_bounds__(512, 1) void istft_kernel(const float2* __restrict_
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int s = s0 + threadIdx.x + 512 * i;
-    if (s < L) yr[s] = wss[i] > 1.17549435e-38f ? acc[i] / wss[i] : acc[i];
+    if (s >= L) continue;
+    const int sp = s + NFFT / 2;
+    const int q = sp / hop;
+    const int fmin = (sp - NFFT) >= 0 ? (sp - NFFT) / hop + 1 : 0;  // first frame covering sp
+    float wss;
+    if (table && fmin == q - K + 1 && q <= T - 1) {
+      wss = wssr[sp - q * hop];
+    } else {
+      wss = 0.f;
+      for (int fr = fmin; fr <= min(q, T - 1); ++fr) {
+        const float w = hann_w(qt, sp - fr * hop);
+        wss += w * w;
+      }
+    }
+    yr[s] = wss > 1.17549435e-38f ? acc[i] / wss : acc[i];
   }
 }
 
@@ -570,12 +628,23 @@ int mst_istft_f32(const float* X, int32_t B, int32_t F, int32_t T, int32_t hop, 
                       (hipStream_t)stream);
 }
 
+// Griffin-Lim runs clip chunks whose spectra and signal (~20 B per bin + 4 B per sample)
+// stay resident in the 256 MB Infinity Cache across the iterations (clips are independent).
+static int gl_chunk(int B, int F, int T, int hop) {
+  const size_t per_clip = (size_t)F * T * 20 + (size_t)hop * (T - 1) * 4;
+  size_t cb = ((size_t)160 << 20) / (per_clip ? per_clip : 1);
+  if (cb < 1) cb = 1;
+  return cb < (size_t)B ? (int)cb : B;
+}
+
 size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t hop) {
-  size_t bins = (size_t)B * F * T;
+  if (B <= 0 || F <= 0 || T <= 1 || hop <= 0) return 0;
+  const int CB = gl_chunk(B, F, T, hop);
+  size_t bins = (size_t)B * F * T, cbins = (size_t)CB * F * T;
   size_t L = (size_t)hop * (T - 1);
-  // St (real) + two complex spectra + signal, each rounded to 256 B
+  // St (real, all clips) + two complex spectra + signal of one chunk, each rounded to 256 B
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
-  return r(bins * 4) + 2 * r(bins * 8) + r((size_t)B * L * 4);
+  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4);
 }
 
 int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
@@ -587,12 +656,13 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   MST_REQUIRE(hop * (T - 1) > NFFT / 2);
   hipStream_t st = (hipStream_t)stream;
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
-  size_t bins = (size_t)B * F * T;
+  const int CB = gl_chunk(B, F, T, hop);
+  const size_t bins = (size_t)B * F * T, cbins = (size_t)CB * F * T;
   char* w = (char*)workspace;
   float* St = (float*)w;
   float2* R0 = (float2*)(w + r(bins * 4));
-  float2* R1 = (float2*)(w + r(bins * 4) + r(bins * 8));
-  float* sig = (float*)(w + r(bins * 4) + 2 * r(bins * 8));
+  float2* R1 = (float2*)(w + r(bins * 4) + r(cbins * 8));
+  float* sig = (float*)(w + r(bins * 4) + 2 * r(cbins * 8));
   const int L = hop * (T - 1);
   {
     dim3 grid(ceil_div(T, 32), ceil_div(F, 32), B), block(32, 8);
@@ -600,21 +670,28 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
     MST_CHECK_LAUNCH();
   }
   const float beta = momentum / (1.f + momentum);
-  // iteration 0 uses the initial phases; iteration 1 has no momentum term (tprev = 0)
-  const float2* cur = reinterpret_cast<const float2*>(angles0);
-  const float2* prev = nullptr;
-  float2* bufs[2] = {R0, R1};
-  int rc;
-  for (int it = 0; it < n_iter; ++it) {
-    rc = istft_launch(cur, prev, St, beta, cur != nullptr, B, T, hop, sig, st);
+  for (int c0 = 0; c0 < B; c0 += CB) {
+    const int nb = min(CB, B - c0);
+    const float* Sc = St + (size_t)c0 * F * T;
+    // iteration 0 uses the initial phases; iteration 1 has no momentum term (tprev = 0)
+    const float2* cur =
+        angles0 ? reinterpret_cast<const float2*>(angles0) + (size_t)c0 * F * T : nullptr;
+    const float2* prev = nullptr;
+    float2* bufs[2] = {R0, R1};
+    int rc;
+    for (int it = 0; it < n_iter; ++it) {
+      rc = istft_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, sig, st);
+      if (rc) return rc;
+      float2* nxt = bufs[it & 1];
+      rc = stft_launch(MODE_COMPLEX, sig, nb, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
+      if (rc) return rc;
+      prev = (it == 0) ? nullptr : cur;
+      cur = nxt;
+    }
+    rc = istft_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, y + (size_t)c0 * L, st);
     if (rc) return rc;
-    float2* nxt = bufs[it & 1];
-    rc = stft_launch(MODE_COMPLEX, sig, B, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
-    if (rc) return rc;
-    prev = (it == 0) ? nullptr : cur;
-    cur = nxt;
   }
-  return istft_launch(cur, prev, St, beta, cur != nullptr, B, T, hop, y, st);
+  return MST_OK;
 }
 
 }  // extern "C"
