@@ -25,6 +25,7 @@
 // shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
 // every loader VALU instruction costs MFMA issue time: the per-element index work is kept
 // wave-uniform (scalar) wherever the mapping allows it.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -508,7 +509,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GP p) {
 int choose_splitk(int M, int N, int nk, int req) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
   const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
-  const double slots = 512.0, tau = 3.4e-6;  // s per 32-deep K tile of one workgroup
+  static const double tau_env = [] {  // dev override for tuning (MST_SPLITK_TAU seconds)
+    const char* e = getenv("MST_SPLITK_TAU");
+    return e ? atof(e) : 0.0;
+  }();
+  const double slots = 512.0;
+  const double tau = tau_env > 0 ? tau_env : 3.4e-6;  // s per 32-deep K tile of one workgroup
   auto waves = [&](long long n) {
     long long full = n / (long long)slots, rem = n % (long long)slots;
     return (double)full + (rem == 0 ? 0.0 : (rem <= slots / 2 ? 0.55 : 1.0));
