@@ -502,6 +502,39 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GP p) {
   }
 }
 
+// Same reduction, four consecutive elements per thread: float4 slab reads, 32-bit index math
+// (host checks M*N % 4 == 0 and M*N < 2^31). Slabs are summed in split order (deterministic,
+// identical to the scalar kernel), four slabs' loads in flight at a time.
+template <bool WG>
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
+  const int total = p.M * p.N;
+  const int q4 = total >> 2;
+  const f32x4* ws = reinterpret_cast<const f32x4*>(p.ws);
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < q4; j += gridDim.x * blockDim.x) {
+    f32x4 v = ws[j];
+    int s = 1;
+    for (; s + 3 <= p.splitk; s += 3) {
+      const f32x4 a = ws[(long long)s * q4 + j], b = ws[(long long)(s + 1) * q4 + j],
+                  c = ws[(long long)(s + 2) * q4 + j];
+      v += a;
+      v += b;
+      v += c;
+    }
+    for (; s < p.splitk; ++s) v += ws[(long long)s * q4 + j];
+    int m = (4 * j) / p.N;
+    int n = 4 * j - m * p.N;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (WG) wgrad_store(p, m, n, v[e]);
+      else conv_store(p, m, n, v[e]);
+      if (++n == p.N) {
+        n = 0;
+        ++m;
+      }
+    }
+  }
+}
+
 // Split-K from a wave-quantisation cost model. 256 CUs x 2 resident workgroups = 512 slots;
 // a workgroup's time is ~ (its K tiles) x tau. A trailing partial wave of <= 256 workgroups
 // runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave. Split-K
@@ -565,9 +598,15 @@ int launch(const GP& p, hipStream_t st, int taps) {
   MST_CHECK_LAUNCH();
   if (p.splitk > 1) {
     long long total = (long long)p.M * p.N;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL((splitk_reduce_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+    if (total % 4 == 0 && total < (1ll << 31)) {
+      int blocks = (int)((total / 4 + 255) / 256);
+      if (blocks > 8192) blocks = 8192;
+      hipLaunchKernelGGL((splitk_reduce4_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+    } else {
+      int blocks = (int)((total + 255) / 256);
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL((splitk_reduce_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+    }
     MST_CHECK_LAUNCH();
   }
   return MST_OK;
