@@ -117,6 +117,8 @@ def main():
     ap.add_argument("--kernel-timing-steps", type=int, default=2)
     ap.add_argument("--no-overlap", action="store_true",
                     help="all-reduce after backward instead of overlapped bucket all-reduces")
+    ap.add_argument("--no-adam-overlap", action="store_true",
+                    help="Adam as one launch in opt.step() instead of per bucket inside backward")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -144,7 +146,10 @@ def main():
     dp.broadcast_parameters(model)
     if world > 1 and not args.no_overlap:
         dp.enable_overlapped_allreduce(model)
-    opt = make_optimizer(model, lr=1e-3)
+    # Adam runs bucket by bucket inside backward, on a side stream, as each bucket's gradients
+    # (and, for N > 1, its all-reduce) complete: the full update, overlapped with the GEMMs
+    opt = make_optimizer(model, lr=1e-3,
+                         overlap_backward=not args.no_adam_overlap and not args.no_overlap)
 
     # synthetic per-rank data, resident in HBM: target clips, style-reference clips, rolls
     tgt_audio, notes = synth_clips(B, 1234 + 1000 * rank)
@@ -164,7 +169,7 @@ def main():
         loss.backward()               # overlapped bucket all-reduces start inside backward
         if world > 1 and args.no_overlap:
             dp.allreduce_gradients(model)
-        opt.step()                    # waits for the all-reduce before the update
+        opt.step()                    # joins the update (or runs it, --no-adam-overlap)
         return loss
 
     for _ in range(args.warmup):

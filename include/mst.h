@@ -25,7 +25,7 @@
  *                            model/model.py:40-53,65-69,81-89   InstanceNorm1d + LeakyReLU(0.01) [+ MaxPool1d(2)]
  *   mst_l1_lrelu_fwd_f32 / _bwd_f32
  *                            model/model.py:299 + model/train.py:132-135,140  lrelu(lastconv) + nn.L1Loss
- *   mst_adam_f32             model/train.py:188,143             optim.Adam(lr=1e-3)
+ *   mst_adam_f32 / _ex_f32   model/train.py:188,143             optim.Adam(lr=1e-3)
  *   mst_onoff_f32            preprocessing/preprocess.py:148-155 piano-roll binarise + onset/offset
  */
 #ifndef MST_H
@@ -93,7 +93,9 @@ typedef struct mst_conv_desc {
   int32_t act;               /* MST_ACT_* */
   float drop_p;              /* 0 = no dropout */
   uint64_t seed;
-  int32_t splitk;            /* 0 = auto */
+  int32_t splitk;            /* K schedule: 0 = auto (split-K or stream-K by a cost model),
+                                n > 0 = split-K over n slabs, -1 = stream-K over one residency
+                                wave (512 workgroups), n < -1 = stream-K over -n workgroups */
   int32_t pad_;
 } mst_conv_desc;
 
@@ -115,7 +117,7 @@ typedef struct mst_wgrad_desc {
   int64_t ldo;
   float scale;
   int32_t accumulate;
-  int32_t splitk;            /* 0 = auto */
+  int32_t splitk;            /* K schedule, as mst_conv_desc.splitk */
   int32_t pad1_;
   int64_t ldc, ldt;          /* output strides per input channel / per tap (0, 0: torch layout) */
 } mst_wgrad_desc;
@@ -174,6 +176,11 @@ int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, fl
  * lr_step = lr / (1 - b1^t); inv_bc2_sqrt = 1/sqrt(1 - b2^t). */
 int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
                  float b2, float eps, float inv_bc2_sqrt, void* stream);
+/* The same update over at most max_blocks 256-thread workgroups (grid-stride): a background
+ * launch beside other kernels (one workgroup per CU leaves the GEMMs their occupancy). */
+int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
+                    float b1, float b2, float eps, float inv_bc2_sqrt, int32_t max_blocks,
+                    void* stream);
 
 /* ---- elementwise helpers ---- */
 int mst_scale_f32(float* x, int64_t n, float s, void* stream);

@@ -25,6 +25,7 @@
 // shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
 // every loader VALU instruction costs MFMA issue time: the per-element index work is kept
 // wave-uniform (scalar) wherever the mapping allows it.
+#include <cmath>
 #include <cstdlib>
 #include <type_traits>
 
@@ -90,7 +91,30 @@ struct GP {
   int accumulate;
   // split-K slab
   float* ws;
+  // stream-K (sk_L > 0): the grid's G workgroups each run sk_L consecutive iterations of the
+  // flattened (tile, 32-deep K tile) space of sk_I = tiles * nk iterations
+  long long sk_L, sk_I;
 };
+
+// Tile-order index -> (M tile, N tile): runs of GM M-tiles x all N-tiles, M fastest within a
+// run, so a contiguous range of indices is a near-square block of tiles (8 x 8 when it holds
+// 64) whose A and B panels are re-read from one L2.
+__device__ __forceinline__ void tile_of(int t2, int nx, int ny, int& m_t, int& n_t) {
+  const int GM = ny < 8 ? ny : 8;
+  const int grp = t2 / (GM * nx);
+  const int fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM;
+  const int tg = t2 - grp * GM * nx;
+  m_t = fm + tg % gm;
+  n_t = tg / gm;
+}
+
+// XCD-aware workgroup numbering. Workgroups are dealt round-robin over the 8 XCDs (linear id
+// % 8), each with its own L2: renumber so every XCD runs one contiguous range of indices.
+__device__ __forceinline__ int xcd_order(int w, int W) {
+  const int q = W >> 3, r = W & 7, xcd = w & 7;
+  return xcd * q + min(xcd, r) + (w >> 3);
+}
 
 __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
   if (m >= p.M || n >= p.N) return;
@@ -163,41 +187,17 @@ __device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
 }
 
+// One pass over K tiles [kt0, kt1) of output tile (m_t, n_t), then the epilogue: the final
+// values (direct), split-K slab `split`, or (slab != nullptr) a stream-K partial tile.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
-__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
-
+__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * LDK], int m_t,
+                                          int n_t, int kt0, int kt1, int split, float* slab) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware tile order. Workgroups are dealt round-robin over the 8 XCDs (linear id % 8),
-  // each with its own L2. Renumber so every XCD runs one contiguous range of tiles: the
-  // workgroups that share A and B panels then sit on one XCD and read them through one L2.
-  int n_t, m_t, split;
-  {
-    const int nx = gridDim.x, ny = gridDim.y;
-    const int W = nx * ny * (int)gridDim.z;
-    const int w = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
-    const int q = W >> 3, r = W & 7, xcd = w & 7;
-    const int t = xcd * q + min(xcd, r) + (w >> 3);
-    // grouped order inside a split: runs of GM M-tiles x all N-tiles, M fastest within a run,
-    // so an XCD's contiguous range is a near-square block of tiles (8 x 8 when it holds 64)
-    // and both its A and its B panels are re-read from the XCD's L2
-    split = t / (nx * ny);
-    const int t2 = t - split * nx * ny;
-    const int GM = ny < 8 ? ny : 8;
-    const int grp = t2 / (GM * nx);
-    const int fm = grp * GM;
-    const int gm = ny - fm < GM ? ny - fm : GM;
-    const int tg = t2 - grp * GM * nx;
-    m_t = fm + tg % gm;
-    n_t = tg / gm;
-  }
   const int n0 = n_t * BN;
   const int m0 = m_t * BM;
-  const int kt0 = (int)((long long)split * p.nk / p.splitk);
-  const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
 
   // Two unit mappings of a 128-row x 32-k tile onto 256 threads, 4 units of 4 consecutive k:
   //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7 -> 8 lanes run along k
@@ -477,13 +477,88 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
       const int m = m0 + ml;
       if (m >= p.M) break;
       const float v = Cs[ml * BN + nl];
-      if (p.splitk > 1) {
+      if (slab) {
+        slab[ml * BN + nl] = v;
+      } else if (p.splitk > 1) {
         p.ws[((long long)split * p.M + m) * p.N + n] = v;
       } else if constexpr (WG) {
         wgrad_store(p, m, n, v);
       } else {
         conv_store(p, m, n, v);
       }
+    }
+  }
+  __syncthreads();  // Cs aliases the A/B buffers the next pass starts writing
+}
+
+// Schedules. Data-parallel / split-K: one (tile, split) per workgroup, grid (nx, ny, splitk).
+// Stream-K: a 1-D grid of G workgroups (one full residency wave); workgroup v runs iterations
+// [v L, v L + L) of the flattened (tile, K tile) space, i.e. the tail of one tile, whole tiles,
+// then the head of another. A tile covered by one workgroup is finished in place; a tile
+// shared by several leaves one partial per workgroup in slab slot 2v (its first tile) or
+// 2v + 1 (its last), which sk_fixup_kernel sums in workgroup order. Every workgroup then does
+// the same work, so there is no partial last wave.
+template <int TAPS, bool WG, int AMODE, bool DUAL>
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  if (p.sk_L == 0) {
+    const int W = nx * ny * (int)gridDim.z;
+    const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
+    const int split = t / (nx * ny);
+    int m_t, n_t;
+    tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
+    const int kt0 = (int)((long long)split * p.nk / p.splitk);
+    const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, nullptr);
+    return;
+  }
+  const int v = xcd_order(blockIdx.x, gridDim.x);
+  long long it = (long long)v * p.sk_L;
+  const long long it1 = it + p.sk_L < p.sk_I ? it + p.sk_L : p.sk_I;
+  int slot = 0;
+  while (it < it1) {
+    const int t = (int)(it / p.nk);
+    const int kt0 = (int)(it - (long long)t * p.nk);
+    const int kt1 = it1 - it < (long long)(p.nk - kt0) ? kt0 + (int)(it1 - it) : p.nk;
+    int m_t, n_t;
+    tile_of(t, nx, ny, m_t, n_t);
+    float* slab = (kt0 == 0 && kt1 == p.nk) ? nullptr
+                                            : p.ws + (long long)(2 * v + slot) * (BM * BN);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, 0, slab);
+    it += kt1 - kt0;
+    slot = 1;
+  }
+}
+
+// Stream-K fixup: one workgroup per (tile, quarter of its rows). A tile finished in place
+// (one covering workgroup) is skipped; otherwise the partials of workgroups v0..v1 are summed
+// in that order (K order) and stored through the normal epilogue.
+template <bool WG>
+__global__ __launch_bounds__(256) void sk_fixup_kernel(const GP p) {
+  const int t = blockIdx.x;
+  const long long L = p.sk_L;
+  const int v0 = (int)((long long)t * p.nk / L);
+  const int v1 = (int)(((long long)(t + 1) * p.nk - 1) / L);
+  if (v0 == v1) return;
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  int m_t, n_t;
+  tile_of(t, nx, ny, m_t, n_t);
+  const int c4 = (threadIdx.x & 31) * 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int ml = blockIdx.y * 32 + (threadIdx.x >> 5) + 8 * r;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int v = v0; v <= v1; ++v) {
+      const int slot = (int)((long long)v * L / p.nk) == t ? 0 : 1;
+      s += *reinterpret_cast<const f32x4*>(p.ws + (long long)(2 * v + slot) * (BM * BN) +
+                                           ml * BN + c4);
+    }
+    const int m = m_t * BM + ml;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (WG) wgrad_store(p, m, n_t * BN + c4 + e, s[e]);
+      else conv_store(p, m, n_t * BN + c4 + e, s[e]);
     }
   }
 }
@@ -566,9 +641,76 @@ int choose_splitk(int M, int N, int nk, int req) {
   return best;
 }
 
+// Stream-K: G workgroups = one residency wave (256 CUs x 2), each ceil(I / G) iterations.
+constexpr int SK_G = 512;
+
+double sk_cost(long long tiles, int nk, int G) {
+  const long long I = tiles * nk;
+  const long long L = (I + G - 1) / G;
+  const double tau = 3.4e-6, seg = 2.0e-6;
+  const double nseg = (double)((L + nk - 1) / nk + 1);
+  const double fixup = L % nk ? (3.0 * G * BM * BN * 4) / 5e12 + 4e-6 : 0.0;
+  return L * tau + nseg * seg + fixup;
+}
+
+// Schedule of one GEMM: req > 0 forces that split-K, req == -1 forces stream-K over SK_G
+// workgroups, req < -1 stream-K over -req workgroups (tests), req == 0 picks the cheaper of
+// the split-K model and stream-K (MST_GEMM_SCHED=dp|sk overrides, for A/B runs).
+void choose_sched(GP& p, int req) {
+  p.sk_L = p.sk_I = 0;
+  const long long tiles = (long long)ceil_div(p.M, BM) * ceil_div(p.N, BN);
+  int G = 0;
+  if (req < 0) {
+    G = req == -1 ? SK_G : -req;
+  } else if (req == 0) {
+    static const int mode = [] {
+      const char* e = getenv("MST_GEMM_SCHED");
+      return !e ? 0 : (e[0] == 's' ? 1 : (e[0] == 'd' ? 2 : 0));
+    }();
+    if (mode == 1) G = SK_G;
+    if (mode == 0) {
+      const int s = choose_splitk(p.M, p.N, p.nk, 0);
+      const double tiles_d = (double)tiles;
+      auto waves = [](double n) {
+        const double full = std::floor(n / 512.0), rem = n - full * 512.0;
+        return full + (rem == 0 ? 0.0 : (rem <= 256.0 ? 0.55 : 1.0));
+      };
+      const double t_split = waves(tiles_d * s) * ceil_div(p.nk, s) * 3.4e-6 +
+                             (s > 1 ? (double)p.M * p.N * 4.0 * (s + 2) / 5e12 + 4e-6 : 0.0);
+      if (sk_cost(tiles, p.nk, SK_G) < t_split * 0.97) G = SK_G;
+    }
+  }
+  if (G > 0) {
+    p.splitk = 1;
+    p.sk_I = tiles * p.nk;
+    p.sk_L = (p.sk_I + G - 1) / G;
+  } else {
+    p.splitk = choose_splitk(p.M, p.N, p.nk, req);
+  }
+}
+
+size_t sched_ws_bytes(const GP& p) {
+  if (p.sk_L > 0) {  // two partial-tile slots per workgroup of the launched grid
+    const long long G = (p.sk_I + p.sk_L - 1) / p.sk_L;
+    return p.sk_L % p.nk ? (size_t)(2 * G) * BM * BN * sizeof(float) : 0;
+  }
+  return p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+}
+
+// Falls back to a single K pass (data-parallel) when the caller's workspace is too small.
+void bind_ws(GP& p, float* ws, size_t ws_bytes) {
+  const size_t need = sched_ws_bytes(p);
+  if (need > 0 && (!ws || ws_bytes < need)) {
+    p.sk_L = p.sk_I = 0;
+    p.splitk = 1;
+  }
+  p.ws = ws;
+}
+
 template <bool WG>
 int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
+  if (p.sk_L > 0) grid = dim3((unsigned)((p.sk_I + p.sk_L - 1) / p.sk_L), 1, 1);
   dim3 block(NTHR);
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
   if (!WG && p.dual)                                                                 \
@@ -596,6 +738,11 @@ int launch(const GP& p, hipStream_t st, int taps) {
 #undef MST_GEMM_CASE
 #undef MST_GEMM_LAUNCH
   MST_CHECK_LAUNCH();
+  if (p.sk_L > 0 && p.sk_L % p.nk) {
+    dim3 fg((unsigned)(p.sk_I / p.nk), BM / 32, 1);
+    hipLaunchKernelGGL((sk_fixup_kernel<WG>), fg, dim3(256), 0, st, p);
+    MST_CHECK_LAUNCH();
+  }
   if (p.splitk > 1) {
     long long total = (long long)p.M * p.N;
     if (total % 4 == 0 && total < (1ll << 31)) {
@@ -696,7 +843,7 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.act = d->act;
   p.drop_p = d->drop_p;
   p.seed = d->seed;
-  p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
+  choose_sched(p, d->splitk);
   return MST_OK;
 }
 
@@ -773,7 +920,7 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
-  p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk);
+  choose_sched(p, d->splitk);
   return MST_OK;
 }
 
@@ -795,18 +942,14 @@ extern "C" {
 size_t mst_conv_fwd_workspace_size(const mst_conv_desc* d) {
   GP p;
   if (build_conv(d, p) != MST_OK) return 0;
-  return p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+  return sched_ws_bytes(p);
 }
 
 int mst_conv_fwd_f32(const mst_conv_desc* d, float* ws, size_t ws_bytes, void* stream) {
   GP p;
   int rc = build_conv(d, p);
   if (rc) return rc;
-  if (p.splitk > 1) {
-    size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
-    if (!ws || ws_bytes < need) p.splitk = 1;  // fall back to a single K pass
-    p.ws = ws;
-  }
+  bind_ws(p, ws, ws_bytes);
   return launch<false>(p, (hipStream_t)stream, d->taps);
 }
 
@@ -820,7 +963,7 @@ size_t mst_wgrad_workspace_size(const mst_wgrad_desc* d) {
   for (int i = 0; i < ns; ++i) {
     GP p;
     if (build_wgrad(d, srcs[i], outs[i], p) != MST_OK) return 0;
-    const size_t w = p.splitk > 1 ? (size_t)p.splitk * p.M * p.N * sizeof(float) : 0;
+    const size_t w = sched_ws_bytes(p);
     need = w > need ? w : need;
   }
   return need;
@@ -839,11 +982,7 @@ int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* ws, size_t ws_bytes, void
   }
   for (int i = 0; i < ns; ++i) {
     GP& p = ps[i];
-    if (p.splitk > 1) {
-      size_t need = (size_t)p.splitk * p.M * p.N * sizeof(float);
-      if (!ws || ws_bytes < need) p.splitk = 1;
-      p.ws = ws;
-    }
+    bind_ws(p, ws, ws_bytes);
     int rc = launch<true>(p, (hipStream_t)stream, d->taps);
     if (rc) return rc;
   }

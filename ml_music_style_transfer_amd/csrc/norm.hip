@@ -551,14 +551,20 @@ int mst_axpby_f32(const float* x, float* y, int64_t n, float a, float b, void* s
   return MST_OK;
 }
 
-int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
-                 float b2, float eps, float bc2_sqrt, void* stream) {
-  MST_REQUIRE(p && g && m && v && n > 0);
+int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
+                    float b1, float b2, float eps, float bc2_sqrt, int32_t max_blocks,
+                    void* stream) {
+  MST_REQUIRE(p && g && m && v && n > 0 && max_blocks > 0);
   MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, 16384)), dim3(256), 0,
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, max_blocks)), dim3(256), 0,
                      (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b1, b2, eps, bc2_sqrt);
   MST_CHECK_LAUNCH();
   return MST_OK;
+}
+
+int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
+                 float b2, float eps, float bc2_sqrt, void* stream) {
+  return mst_adam_ex_f32(p, g, m, v, n, lr_step, b1, b2, eps, bc2_sqrt, 16384, stream);
 }
 
 int mst_scale_f32(float* x, int64_t n, float s, void* stream) {

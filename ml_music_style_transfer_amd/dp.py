@@ -54,6 +54,35 @@ def wait_all(works):
         w.wait()
 
 
+def flat_buckets(model, bucket_bytes):
+    """Cut the model's flat buffers into contiguous buckets of >= bucket_bytes at parameter
+    boundaries, in layout order (= the order backward finishes gradients).
+
+    Returns (buckets: [start, end) element ranges covering [0, n), bucket_of: id(param) ->
+    bucket index, count: parameters per bucket)."""
+    _, _, n = model.flat_buffers()
+    f = model._flat
+    params = model._flat_params_list()
+    spans = sorted((f["index"][id(p)][0], f["index"][id(p)][1], id(p)) for p in params)
+    per = max(1, bucket_bytes // 4)
+    buckets, bucket_of, count = [], {}, []
+    start = 0
+    members = []
+    for i, (o, k, pid) in enumerate(spans):
+        members.append(pid)
+        last = i == len(spans) - 1
+        end = n if last else spans[i + 1][0]
+        if end - start >= per or last:
+            b = len(buckets)
+            buckets.append((start, end))
+            count.append(len(members))
+            for q in members:
+                bucket_of[q] = b
+            members = []
+            start = end
+    return buckets, bucket_of, count
+
+
 class OverlappedAllReduce:
     """Gradient all-reduce overlapped with the backward pass.
 
@@ -72,28 +101,8 @@ class OverlappedAllReduce:
 
     def __init__(self, model, bucket_bytes=OVERLAP_BUCKET_BYTES):
         self.model = model
-        _, grad, n = model.flat_buffers()
-        f = model._flat
-        params = model._flat_params_list()
-        spans = sorted((f["index"][id(p)][0], f["index"][id(p)][1], id(p)) for p in params)
-        per = max(1, bucket_bytes // 4)
-        self.buckets = []     # [start, end) element ranges of the flat gradient buffer
-        self.bucket_of = {}   # id(param) -> bucket index
-        self.count = []       # parameters per bucket
-        start = 0
-        members = []
-        for i, (o, k, pid) in enumerate(spans):
-            members.append(pid)
-            last = i == len(spans) - 1
-            end = n if last else spans[i + 1][0]
-            if end - start >= per or last:
-                b = len(self.buckets)
-                self.buckets.append((start, end))
-                self.count.append(len(members))
-                for q in members:
-                    self.bucket_of[q] = b
-                members = []
-                start = end
+        _, grad, _ = model.flat_buffers()
+        self.buckets, self.bucket_of, self.count = flat_buckets(model, bucket_bytes)
         self.grad = grad
         self.works = []
         self.remaining = list(self.count)

@@ -300,9 +300,11 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
     K.convT1_wgrad(x_dec, dypre, g, acc, scale=MBR_SCALE)
     g, acc = sink.target(P["lastconv.bias"])
     K.bias_grad(dypre, g, acc)
-    sink.block_done()
     dx = torch.empty_like(x_dec)
     K.convT1_dgrad(dypre, W, dx, alpha=MBR_SCALE)
+    # a block is done once its weights are read for the last time (its dgrad): listeners may
+    # then update them (train.BackwardAdam), not just reduce their gradients
+    sink.block_done()
     del dypre
     d_before_m = [None] * depth
     d_before_a = [None] * depth
@@ -378,13 +380,20 @@ class PerformanceNetFunction(torch.autograd.Function):
         module = ctx.module
         P = module._param_dict()
         need = (ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.needs_input_grad[3])
-        reducer = getattr(module, "_mst_dp", None)  # dp.OverlappedAllReduce, if attached
-        if reducer is not None:
-            reducer.begin()
-        sink = module._grad_sink(reducer.ready if reducer is not None else None)
+        # block-completion listeners, in order: dp.OverlappedAllReduce (bucket all-reduces), then
+        # train.BackwardAdam (bucket updates, after their all-reduce)
+        hooks = [h for h in (getattr(module, "_mst_dp", None), getattr(module, "_mst_adam", None))
+                 if h is not None]
+        for h in hooks:
+            h.begin()
+
+        def on_ready(params):
+            for h in hooks:
+                h.ready(params)
+        sink = module._grad_sink(on_ready if hooks else None)
         g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need)
-        if reducer is not None:
-            reducer.launch_remaining()
+        for h in hooks:
+            h.launch_remaining()
         ctx.state = None
         n_params = len(module._flat_params_list())
         return (None, g_m if need[0] else None, g_a if need[1] else None,

@@ -329,9 +329,14 @@ def l1_bwd(pred, target, gscale):
     return dx
 
 
-def adam(p, g, m, v, lr_step, b1, b2, eps, bc2_sqrt):
-    L.check(_lib().mst_adam_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step, b1, b2,
-                                eps, bc2_sqrt, L.stream()), "adam")
+def adam(p, g, m, v, lr_step, b1, b2, eps, bc2_sqrt, max_blocks=None):
+    """max_blocks caps the grid (a background launch beside other kernels)."""
+    if max_blocks is None:
+        L.check(_lib().mst_adam_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step, b1,
+                                    b2, eps, bc2_sqrt, L.stream()), "adam")
+    else:
+        L.check(_lib().mst_adam_ex_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step,
+                                       b1, b2, eps, bc2_sqrt, max_blocks, L.stream()), "adam")
 
 
 def scale_(x, s):

@@ -82,6 +82,38 @@ class Adam(torch.optim.Optimizer):
         self._owner = model
         return self
 
+    def overlap_backward(self, model=None, bucket_bytes=dp.OVERLAP_BUCKET_BYTES):
+        """Run this optimizer's update inside the model's backward pass, bucket by bucket
+        (BackwardAdam). Only for loops that call step() after every backward (the reference's
+        train loop, train.py:131-141): no gradient accumulation across backward passes, no
+        gradient inspection or clipping between backward and step."""
+        if model is not None:
+            self._owner = model
+        self._bwd = BackwardAdam(self, self._owner, bucket_bytes)
+        self._owner._mst_adam = self._bwd
+        return self
+
+    def _flat_state(self, gi, pf, params):
+        key = (gi, pf.data_ptr())
+        st = self._flat_groups.get(key)
+        if st is None:
+            m = torch.zeros_like(pf)
+            v = torch.zeros_like(pf)
+            st = {"m": m, "v": v, "step": 0}
+            self._flat_groups[key] = st
+            index = self._owner._flat["index"]
+            for p in params:
+                o, k = index[id(p)]
+                self.state[p] = {"step": None, "exp_avg": slot_view(m[o:o + k], p),
+                                 "exp_avg_sq": slot_view(v[o:o + k], p)}
+        return st
+
+    def _count_step(self, st, params):
+        st["step"] += 1
+        step_t = torch.tensor(float(st["step"]))
+        for p in params:
+            self.state[p]["step"] = step_t
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
@@ -92,6 +124,10 @@ class Adam(torch.optim.Optimizer):
         reducer = getattr(owner, "_mst_dp", None) if owner is not None else None
         if reducer is not None:
             reducer.finish()  # overlapped data-parallel all-reduce must land first
+        bwd = getattr(self, "_bwd", None)
+        if bwd is not None and bwd.finish():  # the update already ran inside backward
+            self._count_step(bwd.st, bwd.params)
+            return loss
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
             lr, eps = group["lr"], group["eps"]
@@ -101,26 +137,12 @@ class Adam(torch.optim.Optimizer):
             flat = self._flat_of(group, params)
             if flat is not None:
                 pf, gf, n = flat
-                key = (gi, pf.data_ptr())
-                st = self._flat_groups.get(key)
-                if st is None:
-                    m = torch.zeros_like(pf)
-                    v = torch.zeros_like(pf)
-                    st = {"m": m, "v": v, "step": 0}
-                    self._flat_groups[key] = st
-                    index = self._owner._flat["index"]
-                    for p in params:
-                        o, k = index[id(p)]
-                        self.state[p] = {"step": None, "exp_avg": slot_view(m[o:o + k], p),
-                                         "exp_avg_sq": slot_view(v[o:o + k], p)}
-                st["step"] += 1
-                t = st["step"]
+                st = self._flat_state(gi, pf, params)
+                t = st["step"] + 1
                 bc1 = 1 - b1 ** t
                 bc2 = 1 - b2 ** t
                 K.adam(pf, gf, st["m"], st["v"], lr / bc1, b1, b2, eps, math.sqrt(bc2))
-                step_t = torch.tensor(float(t))
-                for p in params:
-                    self.state[p]["step"] = step_t
+                self._count_step(st, params)
                 continue
             for p in params:
                 state = self.state[p]
@@ -138,9 +160,120 @@ class Adam(torch.optim.Optimizer):
         return loss
 
 
-def make_optimizer(model, lr=1e-3):
-    """optim.Adam(model.parameters(), lr=1e-3) (train.py:188) bound to the model's flat buffers."""
-    return Adam(model.parameters(), lr=lr).attach(model)
+class BackwardAdam:
+    """Adam updates issued inside the backward pass, one flat-buffer bucket at a time, on a side
+    stream (Adam.overlap_backward).
+
+    The flat buffers are laid out in the order backward finishes with each parameter
+    (engine.backward_param_order), and the backward program reports a block done only after
+    the block's last read of its weights (its input-gradient GEMM). A bucket whose parameters
+    are all done is final: its update (adam_kernel over the bucket's range: per element the
+    same arithmetic as one launch over the whole buffer) goes to a second stream that waits for
+    the compute stream at that point, so the HBM-bound update runs beside the MFMA-bound
+    backward GEMMs. With the data-parallel reducer attached a bucket's update waits for that
+    bucket's RCCL all-reduce instead. step() then joins the side stream and counts the step.
+
+    Inactive (step() runs the ordinary update) unless one parameter group holds exactly the
+    model's flat parameters, and when gradients are reduced after backward (world > 1 without
+    an overlapped RCCL reducer, or a backend other than NCCL, which averages in finish())."""
+
+    def __init__(self, opt, model, bucket_bytes):
+        self.opt = opt
+        self.model = model
+        reducer = getattr(model, "_mst_dp", None)
+        if reducer is not None:
+            self.buckets, self.bucket_of, self.count = reducer.buckets, reducer.bucket_of, reducer.count
+        else:
+            self.buckets, self.bucket_of, self.count = dp.flat_buckets(model, bucket_bytes)
+        pf, _, _ = model.flat_buffers()
+        self.stream = torch.cuda.Stream(device=pf.device)
+        self.active = self.launched = False
+        self.st = self.params = None
+        self.updates = 0  # steps whose update ran inside backward
+        self.max_blocks = int(os.environ.get("MST_BWD_ADAM_BLOCKS", "256"))  # A/B tuning knob
+
+    def _eligible(self):
+        m = self.model
+        if len(self.opt.param_groups) != 1 or not m._flat_ok():
+            return False
+        # the group may also hold parameters outside the flat buffer (the dead MBR convolutions,
+        # model.py:143-174): backward never gives them a gradient, so Adam skips them anyway
+        index = m._flat["index"]
+        params = [p for p in self.opt.param_groups[0]["params"] if id(p) in index]
+        if len(params) != len(index) or not all(p.requires_grad for p in params):
+            return False
+        if dp.is_dist():
+            reducer = getattr(m, "_mst_dp", None)
+            if reducer is None or reducer.buckets is not self.buckets:
+                return False
+            if torch.distributed.get_backend() != "nccl":
+                return False
+        return True
+
+    def begin(self):
+        self.active = self.launched = False
+        if not self._eligible():
+            return
+        group = self.opt.param_groups[0]
+        index = self.model._flat["index"]
+        self.params = [p for p in group["params"] if id(p) in index]
+        self.pf, self.gf, _ = self.model.flat_buffers()
+        self.st = self.opt._flat_state(0, self.pf, self.params)
+        b1, b2 = group["betas"]
+        t = self.st["step"] + 1
+        self.hp = (group["lr"] / (1 - b1 ** t), b1, b2, group["eps"], math.sqrt(1 - b2 ** t))
+        self.remaining = list(self.count)
+        self.next = 0
+        self.active = True
+
+    def _launch(self, b):
+        s, e = self.buckets[b]
+        reducer = getattr(self.model, "_mst_dp", None)
+        compute = torch.cuda.current_stream()
+        with torch.cuda.stream(self.stream):
+            if reducer is not None and reducer.active:
+                reducer.works[b].wait()  # this stream waits for bucket b's all-reduce
+            else:
+                self.stream.wait_stream(compute)
+            # one workgroup per CU: a background stream beside the backward GEMMs, which keep
+            # their two workgroups per CU (a full-width grid would take their slots instead)
+            K.adam(self.pf[s:e], self.gf[s:e], self.st["m"][s:e], self.st["v"][s:e], *self.hp,
+                   max_blocks=self.max_blocks)
+
+    def ready(self, params):
+        if not self.active:
+            return
+        for p in params:
+            b = self.bucket_of.get(id(p))
+            if b is not None:
+                self.remaining[b] -= 1
+        while self.next < len(self.buckets) and self.remaining[self.next] <= 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def launch_remaining(self):
+        if not self.active:
+            return
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        self.launched = True
+
+    def finish(self):
+        """Join the side stream. True when this backward's update has been issued."""
+        if not (self.active and self.launched):
+            return False
+        torch.cuda.current_stream().wait_stream(self.stream)
+        self.active = self.launched = False
+        self.updates += 1
+        return True
+
+
+def make_optimizer(model, lr=1e-3, overlap_backward=False):
+    """optim.Adam(model.parameters(), lr=1e-3) (train.py:188) bound to the model's flat buffers;
+    overlap_backward=True runs its update inside backward (BackwardAdam)."""
+    opt = Adam(model.parameters(), lr=lr).attach(model)
+    return opt.overlap_backward() if overlap_backward else opt
 
 
 def _cuda(t):

@@ -170,6 +170,40 @@ def test_gemm_splitk(cuda, splitk):
     _close(dW, Wr.grad, B * T, what="splitk wgrad")
 
 
+@pytest.mark.parametrize("sched", [-1, -2, -5, -7, -13, -40])
+def test_gemm_stream_k(cuda, sched):
+    """Stream-K schedules (splitk < 0: -1 = one residency wave of 512 workgroups, else -G
+    workgroups): workgroup ranges start and end inside tiles and inside wgrad time classes,
+    and partial tiles go through the fixup kernel's epilogue (bias + LeakyReLU, accumulate
+    into tap-major weight gradients)."""
+    from ml_music_style_transfer_amd import kernels as K
+    from ml_music_style_transfer_amd import _lib as L
+    B, Cin, Cout, T = 3, 150, 260, 140
+    x, W, b = _r(B, Cin, T, seed=51), _r(Cout, Cin, 3, seed=52), _r(Cout, seed=53)
+    ref = F.leaky_relu(_conv1d_ref(x, W, b), 0.01)
+    xd, Wd, bd = x.float().to(cuda), W.float().to(cuda), b.float().to(cuda)
+    y = torch.full((B, Cout, T), float("nan"), device=cuda)
+    K.conv_like(B=B, M=Cout, Tn=T, srcs=[(xd, 0)], Tv=T, taps=3, a=1, beta=-1, g=1, A=Wd,
+                sAm=Cin * 3, sAc=3, sAt=1, dsts=[(y, 0, None, 1.0)], bias=bd, act=L.ACT_LRELU,
+                splitk=sched)
+    _close(y, ref, Cin * 3, what=f"stream-K fwd {sched}")
+    dy = _r(B, Cout, T, seed=54)
+    Wr = W.clone().requires_grad_(True)
+    _conv1d_ref(x, Wr, None).backward(dy)
+    dW = _tap_major(torch.zeros(Cout, Cin, 3), cuda)
+    for _ in range(2):
+        K.wgrad_like(P=dy.float().to(cuda), srcs=[(xd, 0)], Tv=T, taps=3, a=1, beta=-1, g=1,
+                     out=dW, ldo=dW.stride(0), ldc=dW.stride(1), ldt=dW.stride(2),
+                     accumulate=True, splitk=sched)
+    _close(dW, 2 * Wr.grad, 2 * B * T, what=f"stream-K wgrad {sched}")
+    # deterministic: a second run is bitwise identical
+    y2 = torch.empty_like(y)
+    K.conv_like(B=B, M=Cout, Tn=T, srcs=[(xd, 0)], Tv=T, taps=3, a=1, beta=-1, g=1, A=Wd,
+                sAm=Cin * 3, sAc=3, sAt=1, dsts=[(y2, 0, None, 1.0)], bias=bd, act=L.ACT_LRELU,
+                splitk=sched)
+    assert torch.equal(y, y2)
+
+
 @pytest.mark.parametrize("B", [2, 32])
 def test_conv3_concat_sources_and_split_dsts(cuda, B):
     """Virtual concat with a time offset (crop_and_concat) and a split dgrad destination."""

@@ -219,6 +219,36 @@ def test_train_dropin_runs(cuda):
     assert np.isfinite(tl.item())
 
 
+def test_adam_inside_backward_matches_step(cuda):
+    """BackwardAdam (bucket updates on a side stream during backward) gives bitwise the same
+    parameters, moments and losses as the one-launch update in step(), over three steps with
+    small buckets (many launches, buckets ending inside the network)."""
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd.train import make_optimizer
+    xm, xa, cd, tg = _inputs(2, 44, cuda)
+    runs = []
+    for overlap in (False, True):
+        net = _det_model(cuda).eval()
+        opt = make_optimizer(net, lr=1e-3)
+        if overlap:
+            opt.overlap_backward(bucket_bytes=8 << 20)
+        losses = []
+        for _ in range(3):
+            opt.zero_grad()
+            loss = E.l1_loss(net(xm, xa, cd), tg)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        if overlap:
+            assert opt._bwd.updates == 3 and len(opt._bwd.buckets) > 20
+        pf, _, _ = net.flat_buffers()
+        st = next(iter(opt._flat_groups.values()))
+        runs.append((losses, pf.clone(), st["m"].clone(), st["v"].clone(), st["step"]))
+    (l0, p0, m0, v0, s0), (l1, p1, m1, v1, s1) = runs
+    assert l0 == l1 and s0 == s1 == 3
+    assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
+
+
 def test_backward_gradient_order_matches_flat_layout(cuda):
     """The flat gradient buffer is laid out in engine.backward_param_order so that
     data-parallel buckets complete front to back; check the backward program really
