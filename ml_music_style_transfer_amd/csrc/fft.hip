@@ -15,6 +15,8 @@
 // STFT workgroups: 512 threads (8 waves) x 32 frames of one clip. Results are staged
 // through LDS (reusing the FFT scratch) so each (bin, 32 frames) row of the (B, F, T)
 // output is written as one 128-byte run.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -497,12 +499,24 @@ __global__ __launch_bounds__(512, 2) void istft_kernel(const float2* __restrict_
     const int f = fb + wave;
     if (f <= fhi) {
       const long long base = ((long long)b * T + f) * NB;
+      // Stage the frame's 1025 updated bins in this wave's scratch: each bin is loaded and
+      // phase-updated once (the packed signal below needs bins k and NC - k, which live in
+      // different lanes), and no FFT registers are live yet, so all the loads are in flight
+      // together.
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = lane + 64 * j;
+        S[k] = gl_bin(cur, prev, mag, base, k, beta, norm);
+      }
+      if (lane == 0) S[NC] = gl_bin(cur, prev, mag, base, NC, beta, norm);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       c2 v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int k = lane + 64 * j;
-        c2 Xk = gl_bin(cur, prev, mag, base, k, beta, norm);
-        c2 Xn = gl_bin(cur, prev, mag, base, NC - k, beta, norm);
+        c2 Xk = S[k];
+        c2 Xn = S[NC - k];
         if (k == 0) {
           Xk.y = 0.f;  // irfft ignores the imaginary part of DC and Nyquist
           Xn.y = 0.f;
@@ -511,9 +525,9 @@ __global__ __launch_bounds__(512, 2) void istft_kernel(const float2* __restrict_
         c2 xe = (Xk + Xc) * 0.5f;
         c2 xo = cmul(Xk - Xc, conj(tw_bin(e1, j))) * 0.5f;
         v[j] = xe + mk(-xo.y, xo.x);  // Xe + i Xo
-        // bound the loads in flight (5 floats per bin) so the frame fits 128 VGPRs
-        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // every lane has read the bins before the FFT reuses S
       fft1024<true>(v, S, qt, lane);
       // window (sin^2 form, as the STFT) and 1/NC, in place: S[n] = (x[2n], x[2n+1])
       const c2 eh = eht[lane];
@@ -650,7 +664,11 @@ int mst_istft_f32(const float* X, int32_t B, int32_t F, int32_t T, int32_t hop, 
 // stay resident in the 256 MB Infinity Cache across the iterations (clips are independent).
 static int gl_chunk(int B, int F, int T, int hop) {
   const size_t per_clip = (size_t)F * T * 20 + (size_t)hop * (T - 1) * 4;
-  size_t cb = ((size_t)160 << 20) / (per_clip ? per_clip : 1);
+  static const size_t budget = [] {  // MB; MST_GL_CHUNK_MB overrides (tuning)
+    const char* e = getenv("MST_GL_CHUNK_MB");
+    return (size_t)(e ? atol(e) : 160) << 20;
+  }();
+  size_t cb = budget / (per_clip ? per_clip : 1);
   if (cb < 1) cb = 1;
   return cb < (size_t)B ? (int)cb : B;
 }
