@@ -25,7 +25,6 @@
 // shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
 // every loader VALU instruction costs MFMA issue time: the per-element index work is kept
 // wave-uniform (scalar) wherever the mapping allows it.
-#include <cmath>
 #include <cstdlib>
 #include <type_traits>
 
@@ -644,18 +643,13 @@ int choose_splitk(int M, int N, int nk, int req) {
 // Stream-K: G workgroups = one residency wave (256 CUs x 2), each ceil(I / G) iterations.
 constexpr int SK_G = 512;
 
-double sk_cost(long long tiles, int nk, int G) {
-  const long long I = tiles * nk;
-  const long long L = (I + G - 1) / G;
-  const double tau = 3.4e-6, seg = 2.0e-6;
-  const double nseg = (double)((L + nk - 1) / nk + 1);
-  const double fixup = L % nk ? (3.0 * G * BM * BN * 4) / 5e12 + 4e-6 : 0.0;
-  return L * tau + nseg * seg + fixup;
-}
-
 // Schedule of one GEMM: req > 0 forces that split-K, req == -1 forces stream-K over SK_G
-// workgroups, req < -1 stream-K over -req workgroups (tests), req == 0 picks the cheaper of
-// the split-K model and stream-K (MST_GEMM_SCHED=dp|sk overrides, for A/B runs).
+// workgroups, req < -1 stream-K over -req workgroups (tests), req == 0 uses the split-K cost
+// model (MST_GEMM_SCHED=sk selects stream-K for A/B runs). Stream-K is not chosen
+// automatically: over the training step it was within noise of split-K in time and raised the
+// GEMMs' HBM-side traffic from 254 to 322 MB per launch (profiles/r01/gemm_traffic_m14_*.json):
+// a workgroup walking several tiles in sequence shares fewer panels through L2 with the
+// workgroups running beside it than one tile per workgroup does.
 void choose_sched(GP& p, int req) {
   p.sk_L = p.sk_I = 0;
   const long long tiles = (long long)ceil_div(p.M, BM) * ceil_div(p.N, BN);
@@ -663,22 +657,11 @@ void choose_sched(GP& p, int req) {
   if (req < 0) {
     G = req == -1 ? SK_G : -req;
   } else if (req == 0) {
-    static const int mode = [] {
+    static const bool sk = [] {
       const char* e = getenv("MST_GEMM_SCHED");
-      return !e ? 0 : (e[0] == 's' ? 1 : (e[0] == 'd' ? 2 : 0));
+      return e && e[0] == 's';
     }();
-    if (mode == 1) G = SK_G;
-    if (mode == 0) {
-      const int s = choose_splitk(p.M, p.N, p.nk, 0);
-      const double tiles_d = (double)tiles;
-      auto waves = [](double n) {
-        const double full = std::floor(n / 512.0), rem = n - full * 512.0;
-        return full + (rem == 0 ? 0.0 : (rem <= 256.0 ? 0.55 : 1.0));
-      };
-      const double t_split = waves(tiles_d * s) * ceil_div(p.nk, s) * 3.4e-6 +
-                             (s > 1 ? (double)p.M * p.N * 4.0 * (s + 2) / 5e12 + 4e-6 : 0.0);
-      if (sk_cost(tiles, p.nk, SK_G) < t_split * 0.97) G = SK_G;
-    }
+    if (sk) G = SK_G;
   }
   if (G > 0) {
     p.splitk = 1;
