@@ -579,6 +579,175 @@ __global__ __launch_bounds__(512, 2) void istft_kernel(const float2* __restrict_
   }
 }
 
+// Griffin-Lim's iSTFT in two passes (the workspace holds the windowed frames):
+//   ifft_frames_kernel: one wave per frame, 4 waves per workgroup, no workgroup barriers and
+//     <= 128 VGPRs, so 4 waves/SIMD keep loads and FFTs of different frames overlapped; each
+//     frame is inverse-FFT'd once (the fused istft_kernel recomputes 7 halo frames per
+//     8192-sample segment and runs at 2 waves/SIMD). Writes the windowed, 1/NC-scaled frame.
+//   ola_kernel: every output sample sums its covering frames in increasing order and divides
+//     by the window-sum-square, the same arithmetic in the same order as istft_kernel, so the
+//     two paths agree bitwise.
+constexpr int IFW = 4;  // waves (frames in flight) per ifft_frames workgroup
+
+// gl_bin for bin k = lane + 64 j of one frame through buffer descriptors: the per-lane byte
+// offset is one VGPR and the j part a scalar soffset, so the frame's 48 loads can all be in
+// flight without 48 64-bit addresses (which pushed the kernel past 128 VGPRs into scratch).
+struct FrameBins {
+  __amdgpu_buffer_rsrc_t c, p, m;
+  bool has_c, has_p, has_m, norm;
+  float beta;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t frame_rsrc(const void* ptr, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(ptr), (short)0, bytes, 0x00020000);
+}
+
+__device__ __forceinline__ c2 gl_bin_b(const FrameBins& fb, int lane, int k_sc) {
+  c2 a = mk(1.f, 0.f);
+  if (fb.has_c) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(fb.c, lane * 8, k_sc * 8, 0);
+    a = mk(__builtin_bit_cast(float, (unsigned)u[0]), __builtin_bit_cast(float, (unsigned)u[1]));
+  }
+  if (fb.has_p) {
+    const auto u = __builtin_amdgcn_raw_buffer_load_b64(fb.p, lane * 8, k_sc * 8, 0);
+    a = a - mk(__builtin_bit_cast(float, (unsigned)u[0]), __builtin_bit_cast(float, (unsigned)u[1])) * fb.beta;
+  }
+  if (fb.norm) {
+    const float inv = __builtin_amdgcn_rcpf(sqrtf(a.x * a.x + a.y * a.y) + 1e-16f);
+    a = mk(a.x * inv, a.y * inv);
+  }
+  if (fb.has_m)
+    a = a * __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(fb.m, lane * 4, k_sc * 4, 0));
+  return a;
+}
+constexpr int IFR = 1;  // frames per wave (more: the compiler hoists per-j constants out of the loop and spills)
+
+__global__ __launch_bounds__(256, 4) void ifft_frames_kernel(const float2* __restrict__ cur,
+                                                             const float2* __restrict__ prev,
+                                                             const float* __restrict__ mag,
+                                                             float beta, int normalize, int T,
+                                                             float* __restrict__ frames) {
+  __shared__ __attribute__((aligned(16))) c2 scratch[IFW * SCR];
+  __shared__ c2 qt[QT];
+  __shared__ c2 eht[64];
+  const int b = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  build_qtable(qt);
+  if (threadIdx.x < 64) {
+    double sn, cs;
+    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
+    eht[threadIdx.x] = mk((float)cs, (float)-sn);
+  }
+  __syncthreads();
+  c2* S = scratch + wave * SCR;
+  const bool norm = normalize != 0;
+  const c2 e1 = tw<false>(qt, lane);
+  const c2 eh = eht[lane];
+  const float scale = 1.f / NC;
+#pragma unroll 1
+  for (int r = 0; r < IFR; ++r) {
+    const int f = (blockIdx.x * IFR + r) * IFW + wave;
+    if (f >= T) break;  // wave-uniform; no workgroup barrier follows
+    const long long base = ((long long)b * T + f) * NB;
+    FrameBins fbn;
+    fbn.has_c = cur != nullptr;
+    fbn.has_p = prev != nullptr;
+    fbn.has_m = mag != nullptr;
+    fbn.norm = norm;
+    fbn.beta = beta;
+    fbn.c = frame_rsrc(cur ? cur + base : nullptr, NB * 8);
+    fbn.p = frame_rsrc(prev ? prev + base : nullptr, NB * 8);
+    fbn.m = frame_rsrc(mag ? mag + base : nullptr, NB * 4);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) S[lane + 64 * j] = gl_bin_b(fbn, lane, 64 * j);
+    if (lane == 0) S[NC] = gl_bin_b(fbn, 0, NC);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    // opaque copies: the per-j twiddles and window values are formed where they are used,
+    // not hoisted across the FFT (which would push the kernel past 128 VGPRs)
+    c2 e1a = e1;
+    asm volatile("" : "+v"(e1a.x), "+v"(e1a.y));
+    c2 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = lane + 64 * j;
+      c2 Xk = S[k];
+      c2 Xn = S[NC - k];
+      if (k == 0) {
+        Xk.y = 0.f;
+        Xn.y = 0.f;
+      }
+      c2 Xc = conj(Xn);
+      c2 xe = (Xk + Xc) * 0.5f;
+      c2 xo = cmul(Xk - Xc, conj(tw_bin(e1a, j))) * 0.5f;
+      v[j] = xe + mk(-xo.y, xo.x);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    fft1024<true>(v, S, qt, lane);
+    float2* o = reinterpret_cast<float2*>(frames + ((long long)b * T + f) * NFFT);
+    c2 e1b = e1, ehb = eh;
+    asm volatile("" : "+v"(e1b.x), "+v"(e1b.y), "+v"(ehb.x), "+v"(ehb.y));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int n = lane + 64 * j;
+      const c2 z = S[n];
+      o[n] = make_float2(z.x * (hann_sq(e1b, j) * scale), z.y * (hann_sq(ehb, j) * scale));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // S is restaged by the next frame
+  }
+}
+
+constexpr int OLA_S = 4;  // samples per thread
+
+__global__ __launch_bounds__(256) void ola_kernel(const float* __restrict__ frames, int T, int hop,
+                                                  float* __restrict__ y) {
+  __shared__ c2 qt[QT];
+  __shared__ float wssr[512];
+  const int b = blockIdx.y;
+  const int L = hop * (T - 1);
+  build_qtable(qt);
+  __syncthreads();
+  const int K = NFFT / hop;
+  const bool table = (NFFT % hop) == 0 && hop <= 512;
+  if (table) {
+    for (int r = threadIdx.x; r < hop; r += blockDim.x) {
+      float s = 0.f;
+      for (int k = K - 1; k >= 0; --k) {  // frames in increasing order, as istft_kernel
+        const float w = hann_w(qt, r + hop * k);
+        s += w * w;
+      }
+      wssr[r] = s;
+    }
+  }
+  __syncthreads();
+  const float* fb = frames + (long long)b * T * NFFT;
+  float* yr = y + (long long)b * L;
+#pragma unroll
+  for (int i = 0; i < OLA_S; ++i) {
+    const int s = (blockIdx.x * OLA_S + i) * 256 + threadIdx.x;
+    if (s >= L) break;
+    const int sp = s + NFFT / 2;
+    const int q = sp / hop;
+    const int fmin = (sp - NFFT) >= 0 ? (sp - NFFT) / hop + 1 : 0;
+    const int fmax = min(q, T - 1);
+    float acc = 0.f;
+    for (int fr = fmin; fr <= fmax; ++fr) acc += fb[(long long)fr * NFFT + (sp - fr * hop)];
+    float wss;
+    if (table && fmin == q - K + 1 && q <= T - 1) {
+      wss = wssr[sp - q * hop];
+    } else {
+      wss = 0.f;
+      for (int fr = fmin; fr <= fmax; ++fr) {
+        const float w = hann_w(qt, sp - fr * hop);
+        wss += w * w;
+      }
+    }
+    yr[s] = wss > 1.17549435e-38f ? acc / wss : acc;
+  }
+}
+
 // (B, F, T) -> (B, T, F) with optional log-power -> magnitude (inference.py:109).
 __global__ void transpose_mag_kernel(const float* __restrict__ S, int F, int T, int mag_from_logpow,
                                      float* __restrict__ St) {
@@ -626,6 +795,19 @@ int istft_launch(const float2* cur, const float2* prev, const float* mag, float 
   return MST_OK;
 }
 
+// Two-pass iSTFT through a (B, T, NFFT) frames workspace (Griffin-Lim).
+int istft2_launch(const float2* cur, const float2* prev, const float* mag, float beta,
+                  int normalize, int B, int T, int hop, float* frames, float* y, hipStream_t st) {
+  const int L = hop * (T - 1);
+  hipLaunchKernelGGL(ifft_frames_kernel, dim3(ceil_div(T, IFW * IFR), B), dim3(64 * IFW), 0, st,
+                     cur, prev, mag, beta, normalize, T, frames);
+  MST_CHECK_LAUNCH();
+  hipLaunchKernelGGL(ola_kernel, dim3(ceil_div(L, 256 * OLA_S), B), dim3(256), 0, st, frames, T,
+                     hop, y);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -660,10 +842,11 @@ int mst_istft_f32(const float* X, int32_t B, int32_t F, int32_t T, int32_t hop, 
                       (hipStream_t)stream);
 }
 
-// Griffin-Lim runs clip chunks whose spectra and signal (~20 B per bin + 4 B per sample)
-// stay resident in the 256 MB Infinity Cache across the iterations (clips are independent).
+// Griffin-Lim runs clip chunks whose spectra, frames and signal (~20 B per bin + 8 KB per
+// frame + 4 B per sample) stay resident in the 256 MB Infinity Cache across the iterations
+// (clips are independent).
 static int gl_chunk(int B, int F, int T, int hop) {
-  const size_t per_clip = (size_t)F * T * 20 + (size_t)hop * (T - 1) * 4;
+  const size_t per_clip = (size_t)F * T * 20 + (size_t)T * NFFT * 4 + (size_t)hop * (T - 1) * 4;
   static const size_t budget = [] {  // MB; MST_GL_CHUNK_MB overrides (tuning)
     const char* e = getenv("MST_GL_CHUNK_MB");
     return (size_t)(e ? atol(e) : 160) << 20;
@@ -678,9 +861,10 @@ size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t ho
   const int CB = gl_chunk(B, F, T, hop);
   size_t bins = (size_t)B * F * T, cbins = (size_t)CB * F * T;
   size_t L = (size_t)hop * (T - 1);
-  // St (real, all clips) + two complex spectra + signal of one chunk, each rounded to 256 B
+  // St (real, all clips) + two complex spectra + signal + windowed frames of one chunk, each
+  // rounded to 256 B
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
-  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4);
+  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4);
 }
 
 int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
@@ -700,6 +884,7 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   float2* R1 = (float2*)(w + r(bins * 4) + r(cbins * 8));
   float* sig = (float*)(w + r(bins * 4) + 2 * r(cbins * 8));
   const int L = hop * (T - 1);
+  float* frames = (float*)(w + r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4));
   {
     dim3 grid(ceil_div(T, 32), ceil_div(F, 32), B), block(32, 8);
     hipLaunchKernelGGL(transpose_mag_kernel, grid, block, 0, st, S, F, T, mag_from_logpow, St);
@@ -716,7 +901,7 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
     float2* bufs[2] = {R0, R1};
     int rc;
     for (int it = 0; it < n_iter; ++it) {
-      rc = istft_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, sig, st);
+      rc = istft2_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, frames, sig, st);
       if (rc) return rc;
       float2* nxt = bufs[it & 1];
       rc = stft_launch(MODE_COMPLEX, sig, nb, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
@@ -724,7 +909,8 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
       prev = (it == 0) ? nullptr : cur;
       cur = nxt;
     }
-    rc = istft_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, y + (size_t)c0 * L, st);
+    rc = istft2_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, frames, y + (size_t)c0 * L,
+                       st);
     if (rc) return rc;
   }
   return MST_OK;
