@@ -842,14 +842,16 @@ int mst_istft_f32(const float* X, int32_t B, int32_t F, int32_t T, int32_t hop, 
                       (hipStream_t)stream);
 }
 
-// Griffin-Lim runs clip chunks whose spectra, frames and signal (~20 B per bin + 8 KB per
-// frame + 4 B per sample) stay resident in the 256 MB Infinity Cache across the iterations
-// (clips are independent).
+// Griffin-Lim runs in clip chunks (clips are independent) so the workspace stays bounded for
+// large batches: spectra, windowed frames and signal take ~20 B per bin + 8 KB per frame + 4 B
+// per sample. Chunks sized for the 256 MB Infinity Cache (160 MB) were slower than 2 GB ones
+// once the iSTFT ran as two passes (config 2: 59.9 vs 52.7 ms): filling the chip with
+// workgroups beats cache residency, so the budget is 2 GB (all 256 clips of config 2).
 static int gl_chunk(int B, int F, int T, int hop) {
   const size_t per_clip = (size_t)F * T * 20 + (size_t)T * NFFT * 4 + (size_t)hop * (T - 1) * 4;
   static const size_t budget = [] {  // MB; MST_GL_CHUNK_MB overrides (tuning)
     const char* e = getenv("MST_GL_CHUNK_MB");
-    return (size_t)(e ? atol(e) : 160) << 20;
+    return (size_t)(e ? atol(e) : 2048) << 20;
   }();
   size_t cb = budget / (per_clip ? per_clip : 1);
   if (cb < 1) cb = 1;

@@ -114,11 +114,12 @@ def test_griffinlim_vs_oracle(cuda):
 
 
 def test_griffinlim_clip_chunks(cuda):
-    """Griffin-Lim runs clip chunks sized for the Infinity Cache (160 MB budget): at T = 4000
-    frames a chunk is one clip, so B = 3 runs three chunks; each clip must equal its own B = 1
-    run (bitwise: the kernels are per clip) and the batched y must be in clip order."""
+    """Griffin-Lim runs in clip chunks of at most 2 GB of workspace: at T = 36000 frames
+    (~1.07 GB per clip) a chunk is one clip, so B = 3 runs three chunks; each clip must equal
+    its own B = 1 run (bitwise: the kernels are per clip) and the batched y must be in clip
+    order."""
     from ml_music_style_transfer_amd import spectral
-    B, T = 3, 4000
+    B, T = 3, 36000
     x = (0.1 * np.random.RandomState(20).randn(B, 256 * (T - 1))).astype(np.float32)
     S = spectral.stft_power(torch.from_numpy(x).to(cuda)).clamp_min(0).sqrt()
     y = spectral.griffinlim(S, n_iter=3, init="random", seed=5)
