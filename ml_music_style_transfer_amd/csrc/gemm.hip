@@ -622,6 +622,10 @@ int choose_splitk(int M, int N, int nk, int req) {
   }();
   const double slots = 512.0;
   const double tau = tau_env > 0 ? tau_env : 3.4e-6;  // s per 32-deep K tile of one workgroup
+  static const double bw = [] {  // slab round-trip bandwidth (MST_SPLITK_BW bytes/s, tuning)
+    const char* e = getenv("MST_SPLITK_BW");
+    return e ? atof(e) : 8e12;  // 5e12 -> 8e12: 50.5 -> 50.3 ms/step (sweep 2e12-2e13)
+  }();
   auto waves = [&](long long n) {
     long long full = n / (long long)slots, rem = n % (long long)slots;
     return (double)full + (rem == 0 ? 0.0 : (rem <= slots / 2 ? 0.55 : 1.0));
@@ -631,7 +635,7 @@ int choose_splitk(int M, int N, int nk, int req) {
   const int maxs = nk / 4 < 32 ? nk / 4 : 32;  // at least four K tiles per split
   for (int s = 2; s <= maxs; ++s) {
     const double t = waves(tiles * s) * ceil_div(nk, s) * tau +
-                     (double)M * N * 4.0 * (s + 2) / 5e12 + 4e-6;
+                     (double)M * N * 4.0 * (s + 2) / bw + 4e-6;
     if (t < best_t * 0.97) {
       best_t = t;
       best = s;
