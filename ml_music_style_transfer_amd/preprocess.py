@@ -142,3 +142,22 @@ def piano_roll_from_notes(notes, fs, n_frames=None):
     for p, s, e, v in notes:
         roll[int(p), int(s * fs):int(e * fs)] += v
     return roll
+
+
+def load_midi(midi_path, h=hp, pedal_threshold=64):
+    """preprocess.py:139-160 for one file: pretty_midi piano roll at wps frames/s (restated in
+    midi.py), then binarised roll and onoff on the device. Returns float64 (T, 128) arrays like
+    the reference."""
+    from . import midi as _midi
+    roll = _midi.get_piano_roll(midi_path, fs=h.wps, pedal_threshold=pedal_threshold).T
+    if roll.shape[0] == 0:
+        return np.zeros((0, 128)), np.zeros((0, 128))
+    b, o = pianoroll_onoff(roll)
+    return b.astype(np.float64), o.astype(np.float64)
+
+
+def load_audio(audio_path, h=hp):
+    """librosa.load(path, sr=hp.sr) (preprocess.py:106) via wavio (no resampling)."""
+    from . import wavio
+    y, _ = wavio.load(audio_path, sr=h.sr)
+    return y

@@ -1,0 +1,141 @@
+"""Host-side callers either side of the path: MIDI -> piano roll
+(pretty_midi semantics, midi.py), WAV read/write (librosa.load / soundfile.write, wavio.py)
+and the inference CLI's checkpoint resolution (inference.py:113-124).
+
+pretty_midi, librosa and soundfile are absent here, so the expected values below are
+computed by hand from their published rules: parity unpinned. The SMF bytes are built by
+the small writer in this file, independently of the parser."""
+import json
+import os
+import struct
+import sys
+
+import numpy as np
+import pytest
+
+from ml_music_style_transfer_amd import midi, wavio
+from oracle import midi_ref
+
+
+def _vlq(v):
+    out = [v & 0x7F]
+    v >>= 7
+    while v:
+        out.append(0x80 | (v & 0x7F))
+        v >>= 7
+    return bytes(reversed(out))
+
+
+def _track(events):
+    """events: (abs_tick, raw bytes); delta-encoded, end-of-track appended."""
+    body, last = b"", 0
+    for tick, raw in sorted(events, key=lambda e: e[0]):
+        body += _vlq(tick - last) + raw
+        last = tick
+    body += _vlq(0) + b"\xff\x2f\x00"
+    return b"MTrk" + struct.pack(">I", len(body)) + body
+
+
+def _smf(tracks, division=480, fmt=1):
+    return b"MThd" + struct.pack(">IHHH", 6, fmt, len(tracks), division) + b"".join(tracks)
+
+
+def _tempo(bpm):
+    us = int(round(6e7 / bpm))
+    return b"\xff\x51\x03" + bytes([(us >> 16) & 255, (us >> 8) & 255, us & 255])
+
+
+def _on(ch, p, v):
+    return bytes([0x90 | ch, p, v])
+
+
+def _off(ch, p):
+    return bytes([0x80 | ch, p, 0])
+
+
+def test_tempo_map_and_roll():
+    """Tempo from track 0 (120 bpm, then 60 bpm at tick 960); notes on track 1."""
+    t0 = _track([(0, _tempo(120)), (960, _tempo(60))])
+    t1 = _track([(0, b"\xc0\x00"), (0, _on(0, 60, 100)), (480, _off(0, 60)),
+                 (720, _on(0, 64, 80)), (1440, _off(0, 64))])
+    m = midi.MidiFile(_smf([t0, t1]))
+    notes = sorted(((n.pitch, n.start, n.end, n.velocity) for i in m.instruments for n in i.notes))
+    # 120 bpm: 480 ticks = 0.5 s; after tick 960 (1.0 s) 60 bpm: 480 ticks = 1.0 s
+    assert notes == [(60, 0.0, 0.5, 100), (64, 0.75, 2.0, 80)]
+    roll = m.get_piano_roll(fs=172)
+    np.testing.assert_array_equal(roll, midi_ref.piano_roll(notes, 172))
+    assert roll.shape == (128, int(172 * 2.0))
+
+
+def test_note_off_rules_and_running_status():
+    """A note-off closes every open note of its (channel, pitch) not started on the same tick;
+    note-on velocity 0 is a note-off; running status; unclosed notes are dropped."""
+    raw = (_vlq(0) + bytes([0x90, 60, 90]) + _vlq(100) + bytes([60, 70])  # running status
+           + _vlq(100) + bytes([60, 0])                                      # vel-0 off at 200
+           + _vlq(0) + bytes([62, 50])                                       # on 62 at 200
+           + _vlq(0) + b"\xff\x2f\x00")
+    tr = b"MTrk" + struct.pack(">I", len(raw)) + raw
+    m = midi.MidiFile(_smf([tr], division=100, fmt=0))
+    notes = sorted((n.pitch, n.start, n.end, n.velocity) for i in m.instruments for n in i.notes)
+    # 100 ticks per beat at 120 bpm: 1 tick = 5 ms. Both 60s close at tick 200; 62 never closes.
+    assert notes == [(60, 0.0, 1.0, 90), (60, 0.5, 1.0, 70)]
+    same_tick = _track([(0, _on(0, 60, 90)), (100, _on(0, 60, 70)), (100, _off(0, 60)),
+                        (300, _off(0, 60))])
+    m = midi.MidiFile(_smf([same_tick], division=100))
+    notes = sorted((n.start, n.end, n.velocity) for i in m.instruments for n in i.notes)
+    assert notes == [(0.0, 0.5, 90), (0.5, 1.5, 70)]
+
+
+def test_sustain_pedal_and_drums():
+    fs = 100
+    tr = _track([(0, _on(0, 60, 100)), (48, _off(0, 60)),          # 0 .. 0.05 s
+                 (24, bytes([0xB0, 64, 127])), (480, bytes([0xB0, 64, 0])),  # pedal .025-.5 s
+                 (0, _on(9, 36, 120)), (960, _off(9, 36))])          # drum to 1.0 s
+    m = midi.MidiFile(_smf([tr]))
+    assert sorted(i.is_drum for i in m.instruments) == [False, True]
+    roll = m.get_piano_roll(fs=fs)
+    assert roll.shape == (128, 100)          # the drum extends the length, adds nothing
+    assert roll[36].sum() == 0
+    expect = np.zeros(100)
+    expect[0:50] = 100                        # held by the pedal from frame 2 to frame 50
+    np.testing.assert_array_equal(roll[60], expect)
+    np.testing.assert_array_equal(m.get_piano_roll(fs=fs, pedal_threshold=None)[60][:10],
+                                  np.r_[np.full(5, 100.0), np.zeros(5)])
+
+
+def test_midi_errors():
+    with pytest.raises(ValueError):
+        midi.MidiFile(b"RIFF....")
+    with pytest.raises(ValueError):
+        midi.MidiFile(b"MThd" + struct.pack(">IHHH", 6, 0, 1, 0xE728))  # SMPTE
+
+
+def test_wav_roundtrip_and_formats(tmp_path):
+    rng = np.random.default_rng(0)
+    y = (0.9 * np.sin(np.arange(4410) * 0.05) + 0.01 * rng.standard_normal(4410)).astype(np.float32)
+    p = str(tmp_path / "a.wav")
+    wavio.write(p, y, 44100)
+    r, sr = wavio.load(p, sr=44100)
+    assert sr == 44100 and r.dtype == np.float32 and r.shape == y.shape
+    # libsndfile scales: write x * 0x7FFF, read int / 0x8000
+    np.testing.assert_array_equal(r, (np.rint(y.astype(np.float64) * 32767) / 32768).astype(np.float32))
+    wavio.write(p, np.array([2.0, -2.0], np.float32), 44100)
+    np.testing.assert_array_equal(wavio.load(p)[0], np.array([32767, -32768]) / 32768.0)
+    # stereo 24-bit PCM -> mono mean
+    raw = np.array([[1 << 22, -(1 << 22)], [1 << 21, 1 << 21]], np.int32)
+    b = b"".join(int(v & 0xFFFFFF).to_bytes(3, "little") for v in raw.ravel())
+    fmt = struct.pack("<HHIIHH", 1, 2, 44100, 44100 * 6, 6, 24)
+    wav = b"RIFF" + struct.pack("<I", 4 + 8 + 16 + 8 + len(b)) + b"WAVE" + b"fmt " + \
+        struct.pack("<I", 16) + fmt + b"data" + struct.pack("<I", len(b)) + b
+    q = tmp_path / "b.wav"
+    q.write_bytes(wav)
+    np.testing.assert_allclose(wavio.load(str(q))[0], [0.0, 0.25])
+    with pytest.raises(ValueError):
+        wavio.load(str(q), sr=16000)
+
+
+def test_best_checkpoint_name(tmp_path):
+    from ml_music_style_transfer_amd import inference
+    with open(tmp_path / "hyperparams.json", "w") as f:
+        json.dump({"best_epoch": 7, "best_loss": 0.5}, f)
+    assert inference.best_checkpoint_name(str(tmp_path)) == "checkpoint-7.tar"
