@@ -8,9 +8,10 @@ is a torch.optim.Optimizer whose step runs one fused kernel over the model's
 flat parameter buffer (torch.optim.Adam semantics, state_dict format included,
 so ReduceLROnPlateau and checkpointing work unchanged).
 
-The HDF5 data path (Dataseth5py / Process_Data, train.py:45-116) needs h5py,
-which this image lacks: `SyntheticSpectrogramDataset` produces batches of the
-same (data (B,256,T), data_cond (B,1025,T), target (B,1025,T)) shape instead.
+The HDF5 data path (Dataseth5py / Process_Data, train.py:45-116) is in data.py
+(libhdf5 through ctypes; h5py is absent). `SyntheticSpectrogramDataset` produces
+batches of the same (data (B,256,T), data_cond (B,1025,T), target (B,1025,T))
+shape when no HDF5 files are given.
 """
 import argparse
 import json
@@ -340,7 +341,8 @@ class SyntheticSpectrogramDataset(torch.utils.data.Dataset):
 
 
 def main(args):
-    """train.py:173-208 with the synthetic dataset standing in for HDF5."""
+    """train.py:173-208. Reads `<data_dir>_train.hdf5` / `_test.hdf5` (data.Process_Data,
+    HBM-resident loaders) when they exist, else a synthetic dataset of the same layout."""
     hp = hyperparams(args)
     exp_root = os.path.join(os.path.abspath('./'), 'experiments')
     os.makedirs(exp_root, exist_ok=True)
@@ -351,11 +353,18 @@ def main(args):
     model.zero_grad()
     optimizer.zero_grad()
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, 'min')
-    T = args.frames
-    train_ds = SyntheticSpectrogramDataset(args.n_train_read or 32, T=T, seed=1)
-    test_ds = SyntheticSpectrogramDataset(args.n_test_read or 8, T=T, seed=2)
-    train_loader = torch.utils.data.DataLoader(train_ds, batch_size=args.batch_size, shuffle=True)
-    test_loader = torch.utils.data.DataLoader(test_ds, batch_size=args.batch_size)
+    if args.data_dir and os.path.exists(args.data_dir + '_train.hdf5'):
+        from .data import Process_Data
+        train_loader, test_loader = Process_Data(args.data_dir, n_train_read=args.n_train_read,
+                                                 n_test_read=args.n_test_read,
+                                                 batch_size=args.batch_size)
+    else:
+        T = args.frames
+        train_ds = SyntheticSpectrogramDataset(args.n_train_read or 32, T=T, seed=1)
+        test_ds = SyntheticSpectrogramDataset(args.n_test_read or 8, T=T, seed=2)
+        train_loader = torch.utils.data.DataLoader(train_ds, batch_size=args.batch_size,
+                                                   shuffle=True)
+        test_loader = torch.utils.data.DataLoader(test_ds, batch_size=args.batch_size)
     print('start training')
     for epoch in range(hp.train_epoch):
         loss = train(model, epoch, train_loader, optimizer, hp.iter_train_loss)
@@ -377,7 +386,8 @@ def main(args):
 
 def parse_args(argv=None):
     parser = argparse.ArgumentParser()
-    parser.add_argument("-data-dir", type=str, default='', help="(HDF5 path; synthetic data here)")
+    parser.add_argument("-data-dir", type=str, default='',
+                        help="HDF5 prefix (<dir>_train.hdf5); synthetic data when absent")
     parser.add_argument("-epochs", type=int, default=1)
     parser.add_argument("-test-freq", type=int, default=1)
     parser.add_argument("-exp-name", type=str, default='piano_test')

@@ -80,3 +80,56 @@ def test_inference_cli_end_to_end(cuda, tmp_path, monkeypatch):
     expect = (np.clip(np.rint(y.astype(np.float64) * 32767), -32768, 32767) / 32768).astype(np.float32)
     np.testing.assert_array_equal(got, expect)
     assert np.isfinite(y).all() and np.abs(y).max() > 0
+
+
+def test_device_loader_on_gpu_matches_dataloader(cuda, tmp_path):
+    """data.DeviceLoader (split resident in HBM, batches gathered on the device) yields the
+    DataLoader(Dataseth5py) batches bit for bit."""
+    from ml_music_style_transfer_amd import data
+    rng = np.random.default_rng(4)
+    N, T = 9, 44
+    pr = (rng.random((N, T, 128)) < 0.1).astype(float)
+    oo = np.diff(np.concatenate([np.zeros((N, 1, 128)), pr], 1), axis=1)
+    data.write_split(str(tmp_path / "d_train.hdf5"), pr, oo,
+                     {s: rng.random((N, 1025, T)) for s in ("cuba", "harpsichord", "upright")})
+    torch.manual_seed(11)
+    dl = torch.utils.data.DataLoader(data.Dataseth5py(str(tmp_path / "d_train.hdf5")),
+                                     batch_size=4, shuffle=True)
+    ref = [[t.clone() for t in b] for b in dl]
+    torch.manual_seed(11)
+    got = list(data.DeviceLoader(data.Dataseth5py(str(tmp_path / "d_train.hdf5")), batch_size=4,
+                                 shuffle=True))
+    assert len(got) == len(ref) == 3
+    for r, g in zip(ref, got):
+        for a, b in zip(r, g):
+            assert b.is_cuda and torch.equal(a, b.cpu())
+
+
+def test_hdf5_train_checkpoint_then_inference(cuda, tmp_path, monkeypatch):
+    """train.main on `<data_dir>_train/_test.hdf5` (train.py:173-208) -> checkpoint-1.tar +
+    hyperparams.json -> inference.main on the best epoch (inference.py:113-124)."""
+    from ml_music_style_transfer_amd import data, inference, wavio
+    from ml_music_style_transfer_amd import train as TR
+    monkeypatch.chdir(tmp_path)
+    rng = np.random.default_rng(5)
+    for split, N in (("train", 4), ("test", 2)):
+        T = 44
+        pr = (rng.random((N, T, 128)) < 0.1).astype(float)
+        oo = np.diff(np.concatenate([np.zeros((N, 1, 128)), pr], 1), axis=1)
+        data.write_split(str(tmp_path / ("piano_%s.hdf5" % split)), pr, oo,
+                         {"cuba": 2 * rng.random((N, 1025, T)), "upright": 2 * rng.random((N, 1025, T))})
+    hp = TR.main(TR.parse_args(["-data-dir", str(tmp_path / "piano"), "-epochs", "1",
+                                "--batch-size", "2"]))
+    exp_dir = tmp_path / "experiments" / "piano_test"
+    assert hp.best_epoch == 1 and np.isfinite(hp.loss_history).all()
+    assert (exp_dir / "checkpoint-1.tar").exists()
+    with open(exp_dir / "hyperparams.json") as f:
+        assert json.load(f)["best_epoch"] == 1
+    (exp_dir / "midi").mkdir()
+    (exp_dir / "midi" / "score.mid").write_bytes(_smf_two_notes())
+    t = np.arange(int(0.6 * 44100)) / 44100.0
+    wavio.write(str(tmp_path / "style.wav"), 0.3 * np.sin(2 * np.pi * 220 * t), 44100)
+    paths = inference.main(["-exp-name", "piano_test", "-midi-source", "score.mid",
+                            "-audio-source", str(tmp_path / "style.wav"), "--n-iter", "2"])
+    y, sr = wavio.load(paths[0])
+    assert sr == 44100 and y.shape == (256 * (16 * (103 // 16) + 12 - 1),) and np.isfinite(y).all()

@@ -139,3 +139,77 @@ def test_best_checkpoint_name(tmp_path):
     with open(tmp_path / "hyperparams.json", "w") as f:
         json.dump({"best_epoch": 7, "best_loss": 0.5}, f)
     assert inference.best_checkpoint_name(str(tmp_path)) == "checkpoint-7.tar"
+
+
+# ---------------------------------------------------------------- HDF5 data path (§8(f) #1)
+def _split(rng, N=7, T=20, styles=("cuba", "upright")):
+    pr = (rng.random((N, T, 128)) < 0.1).astype(float)
+    oo = np.diff(np.concatenate([np.zeros((N, 1, 128)), pr], 1), axis=1)
+    return pr, oo, {s: rng.random((N, 1025, T)) for s in styles}
+
+
+def test_hdf5_schema_roundtrip_and_append(tmp_path):
+    """io_manager.h5pyManager's layout: float64, chunked, resizable on axis 0, appended."""
+    from ml_music_style_transfer_amd import h5
+    rng = np.random.default_rng(1)
+    a, b = rng.random((3, 20, 128)), rng.random((2, 20, 128))
+    p = str(tmp_path / "x.hdf5")
+    with h5.File(p, "w") as f:
+        f.create_dataset("pianoroll", data=a, dtype="float64", maxshape=(None, 20, 128), chunks=True)
+        d = f["pianoroll"]
+        d.resize(d.shape[0] + b.shape[0], axis=0)
+        d[-b.shape[0]:] = b
+    with h5.File(p) as f:
+        assert f.keys() == ["pianoroll"] and "pianoroll" in f and "onoff" not in f
+        assert f["pianoroll"].shape == (5, 20, 128)
+        np.testing.assert_array_equal(f["pianoroll"][:], np.concatenate([a, b]))
+        np.testing.assert_array_equal(f["pianoroll"][:100], np.concatenate([a, b]))  # n_read > n
+        np.testing.assert_array_equal(f["pianoroll"][3], b[0])
+        with pytest.raises(KeyError):
+            f["spec_cuba"]
+
+
+def test_dataset_item_rule(tmp_path):
+    """Dataseth5py.__getitem__ (train.py:74-99): concat+transpose, random style, random cond."""
+    import random
+    from ml_music_style_transfer_amd import data
+    rng = np.random.default_rng(2)
+    pr, oo, specs = _split(rng)
+    data.write_split(str(tmp_path / "d_train.hdf5"), pr, oo, specs)
+    ds = data.Dataseth5py(str(tmp_path / "d_train.hdf5"), n_read=5)
+    assert ds.styles == ["spec_cuba", "spec_upright"] and len(ds) == 5
+    random.seed(42)
+    expect = []
+    for i in (0, 4, 2):
+        style = random.choice(ds.styles)
+        r = random.randint(0, 4)
+        expect.append((midi_ref.assemble_item(pr[i], oo[i]), specs[style[5:]][r], specs[style[5:]][i]))
+    random.seed(42)
+    for i, (eX, eC, eY) in zip((0, 4, 2), expect):
+        X, Xc, y = ds[i]
+        np.testing.assert_array_equal(X.numpy(), eX.astype(np.float32))
+        np.testing.assert_array_equal(Xc.numpy(), eC.astype(np.float32))
+        np.testing.assert_array_equal(y.numpy(), eY.astype(np.float32))
+
+
+def test_device_loader_reproduces_dataloader(tmp_path):
+    """DeviceLoader == DataLoader(Dataseth5py, shuffle=True) batch for batch over two epochs
+    (same torch and random seeds); checked on CPU tensors here, on the GPU in
+    test_gpu_inference.py."""
+    import torch
+    from ml_music_style_transfer_amd import data
+    pr, oo, specs = _split(np.random.default_rng(3))
+    data.write_split(str(tmp_path / "d_train.hdf5"), pr, oo, specs)
+    for shuffle in (True, False):
+        torch.manual_seed(5)
+        ds = data.Dataseth5py(str(tmp_path / "d_train.hdf5"))
+        dl = torch.utils.data.DataLoader(ds, batch_size=3, shuffle=shuffle)
+        ref = [[t.clone() for t in b] for _ in range(2) for b in dl]
+        torch.manual_seed(5)
+        dl2 = data.DeviceLoader(data.Dataseth5py(str(tmp_path / "d_train.hdf5")), batch_size=3,
+                                shuffle=shuffle, device="cpu")
+        got = [b for _ in range(2) for b in dl2]
+        assert len(dl2) == len(dl) == 3 and len(got) == len(ref) == 6
+        for r, g in zip(ref, got):
+            for a, b in zip(r, g):
+                assert torch.equal(a, b)
