@@ -22,7 +22,7 @@ import torch
 
 from . import h5
 
-__all__ = ["Dataseth5py", "Process_Data", "DeviceLoader", "write_split"]
+__all__ = ["Dataseth5py", "Process_Data", "DeviceLoader", "write_split", "h5pyManager"]
 
 
 class Dataseth5py(torch.utils.data.Dataset):
@@ -122,3 +122,28 @@ def write_split(path, pianoroll, onoff, specs):
             a = np.asarray(arr, np.float64)
             f.create_dataset(name, data=a, dtype='float64', maxshape=(None,) + a.shape[1:],
                              chunks=True)
+
+
+class h5pyManager():
+    """preprocessing/utils/io_manager.py:39-76: create on first write, then resize on axis 0
+    and append, so pianoroll[i] / onoff[i] / spec_<style>[i] line up."""
+
+    def __init__(self, data):
+        self.data = data
+
+    def _append(self, name, arr):
+        arr = np.asarray(arr, np.float64)
+        if name not in self.data:
+            self.data.create_dataset(name, data=arr, dtype='float64',
+                                     maxshape=(None,) + arr.shape[1:], chunks=True)
+        else:
+            d = self.data[name]
+            d.resize(d.shape[0] + arr.shape[0], axis=0)
+            d[-arr.shape[0]:] = arr
+
+    def write_pianoroll(self, pianoroll_list, onoff_list):
+        self._append("pianoroll", pianoroll_list)
+        self._append("onoff", onoff_list)
+
+    def write_spectrum(self, spec_list, style):
+        self._append(f'spec_{style}', spec_list)

@@ -29,7 +29,7 @@ from . import spectral
 from . import wavio
 from .model import PerformanceNet
 from .preprocess import hp as pp_hp
-from .preprocess import load_audio, load_midi, process_spectrum_from_chunk
+from .preprocess import midi_file_to_roll, process_spectrum_from_chunk, read_audio
 
 
 def load_checkpoint(path):
@@ -70,8 +70,8 @@ class AudioSynthesizer():
         device. The score (wps frames/s) and the audio (1 + L//256 frames) rarely have the same
         length; the reference leaves that as a TODO (inference.py:62-68, its forward then fails
         in the first DenseConcat), here both are cut to the shorter one."""
-        pianoroll, onoff = load_midi(os.path.join(self.exp_dir, 'midi', midi_filename))
-        audio = load_audio(audio_filename)
+        pianoroll, onoff = midi_file_to_roll(os.path.join(self.exp_dir, 'midi', midi_filename))
+        audio = read_audio(audio_filename)
         spec = process_spectrum_from_chunk(torch.from_numpy(audio).cuda())
         T = min(pianoroll.shape[0], spec.shape[1])
         pianoroll = torch.from_numpy(pianoroll[:T].T.astype(np.float32)).cuda().unsqueeze(0)

@@ -4,9 +4,12 @@
 same (1025, 1 + L//256) float32 array type it was given (NumPy in -> NumPy out,
 CUDA tensor in -> CUDA tensor out); the STFT itself always runs in libmst_hip.
 The integer chunk/frame arithmetic is the reference's, bit for bit.
-File globbing, zip extraction, librosa.load/pretty_midi file parsing and HDF5
-writing (preprocess.py:99-116,139-147,163-214) are offline I/O outside this path.
+`load_midi` / `load_audio` / `get_data` / `main` (preprocess.py:99-215) keep the
+reference's signatures: file globbing as the reference, pretty_midi and librosa.load
+restated in midi.py / wavio.py, HDF5 written through h5.py.
 """
+import glob
+
 import numpy as np
 import torch
 
@@ -144,10 +147,11 @@ def piano_roll_from_notes(notes, fs, n_frames=None):
     return roll
 
 
-def load_midi(midi_path, h=hp, pedal_threshold=64):
-    """preprocess.py:139-160 for one file: pretty_midi piano roll at wps frames/s (restated in
-    midi.py), then binarised roll and onoff on the device. Returns float64 (T, 128) arrays like
-    the reference."""
+
+def midi_file_to_roll(midi_path, h=hp, pedal_threshold=64):
+    """The body of preprocess.py:146-155 for one file: pretty_midi piano roll at wps frames/s
+    (restated in midi.py), then the binarised roll and onoff on the device. Returns float64
+    (T, 128) arrays like the reference."""
     from . import midi as _midi
     roll = _midi.get_piano_roll(midi_path, fs=h.wps, pedal_threshold=pedal_threshold).T
     if roll.shape[0] == 0:
@@ -156,8 +160,96 @@ def load_midi(midi_path, h=hp, pedal_threshold=64):
     return b.astype(np.float64), o.astype(np.float64)
 
 
-def load_audio(audio_path, h=hp):
+def read_audio(audio_path, h=hp):
     """librosa.load(path, sr=hp.sr) (preprocess.py:106) via wavio (no resampling)."""
     from . import wavio
     y, _ = wavio.load(audio_path, sr=h.sr)
     return y
+
+
+def _one_file(pattern, what):
+    files = glob.glob(pattern)
+    if len(files) == 0:
+        raise ValueError("couldnt find %s track!" % what)
+    elif len(files) > 1:
+        raise ValueError("multiple files picked up, issue:", files)
+    return files[0]
+
+
+def load_audio(data_dir, song_id, style, debug=False, h=hp):
+    """preprocess.py:99-115."""
+    path = _one_file(f"{data_dir}/{song_id}*{style}.wav", "audio")
+    y = read_audio(path, h)
+    if debug is True:
+        print("length of audio clip / sr: ", len(y), h.sr)
+        print("audio files picked up:", [path])
+    return y
+
+
+def load_midi(data_dir, song_id, ext='mixcraft', debug=False, h=hp):
+    """preprocess.py:139-160."""
+    path = _one_file(f"{data_dir}/{song_id}*{ext}.mid", "midi")
+    pianoroll, onoff = midi_file_to_roll(path, h)
+    if debug is True:
+        print("length of pianoroll: ", pianoroll.shape)
+        print("midi files picked up:", [path])
+    return pianoroll, onoff
+
+
+def get_data(data_dir, dataset_outpath, data_type, debug=False, h=hp):
+    """preprocess.py:163-200: every song of hp.piano_scores[data_type] -> pianoroll/onoff
+    chunks and, per style whose audio exists, log-power spectrogram chunks (one batched STFT
+    launch per song and style), appended to `<dataset_outpath>_<data_type>.hdf5`
+    (io_manager.h5pyManager layout, data.h5pyManager). Like the reference, a missing style
+    is skipped for that song."""
+    from . import h5
+    from .data import h5pyManager
+    h5name = f"{dataset_outpath}_{data_type}.hdf5"
+    with h5.File(h5name, 'w') as h5_data:
+        manager = h5pyManager(h5_data)
+        for song_id in h.piano_scores[data_type]:
+            pianoroll, onoff = load_midi(data_dir, song_id, debug=debug, h=h)
+            num_chunks = get_num_song_chunks(pianoroll, h=h)
+            pianoroll_list, onoff_list = process_pianoroll_into_chunks(pianoroll, onoff, song_id,
+                                                                       num_chunks, debug=debug, h=h)
+            manager.write_pianoroll(pianoroll_list, onoff_list)
+            for style in h.styles:
+                try:
+                    audio = load_audio(data_dir, song_id, style, debug=debug, h=h)
+                except (ValueError, OSError):
+                    print(f"Couldnt load audio for song={song_id}, style={style}, skipping...")
+                    continue
+                spec_list = process_audio_into_chunks(audio, style, song_id, num_chunks,
+                                                      debug=debug, h=h)
+                manager.write_spectrum(np.asarray(spec_list, dtype=np.float64), style)
+    return h5name
+
+
+def main(args):
+    """preprocess.py:203-215 (zip extraction, then get_data)."""
+    import os
+    import zipfile
+    if zipfile.is_zipfile(args.data_dir) is True:
+        print("Extracting zip file to local")
+        cwd = os.getcwd()
+        with zipfile.ZipFile(args.data_dir, 'r') as zip_ref:
+            root_data_dir = os.path.dirname(zip_ref.namelist()[0])
+            zip_ref.extractall(cwd)
+        args.data_dir = os.path.join(cwd, root_data_dir)
+    return get_data(args.data_dir, args.dataset_outpath, args.data_type, args.debug)
+
+
+def parse_args(argv=None):
+    import argparse
+    parser = argparse.ArgumentParser()
+    parser.add_argument("-data-dir", type=str, required=True)
+    parser.add_argument("-dataset-outpath", type=str, required=True)
+    parser.add_argument("-max-chunks-per-song", type=int, default=100)
+    parser.add_argument("-data-type", type=str, default='train', choices=['train', 'test'])
+    parser.add_argument("--debug", type=lambda v: str(v).lower() in ('yes', 'true', 't', 'y', '1'),
+                        default=False)
+    return parser.parse_args(argv)
+
+
+if __name__ == "__main__":
+    main(parse_args())
