@@ -81,6 +81,98 @@ def istft(X, hop=256):
     return y[0] if single else y
 
 
+# ------------------------------------------------- differentiable iSTFT (training losses)
+_WSS_CACHE = {}
+
+
+def _inv_wss(T, hop, n_fft, device):
+    """1 / window-sum-square at the kept (center-trimmed) samples, 0 where it vanishes."""
+    key = (T, hop, n_fft, str(device))
+    if key not in _WSS_CACHE:
+        n = torch.arange(n_fft, dtype=torch.float64)
+        w2 = (0.5 - 0.5 * torch.cos(2 * math.pi * n / n_fft)) ** 2
+        wss = torch.zeros(n_fft + hop * (T - 1), dtype=torch.float64)
+        for k in range(T):
+            wss[k * hop:k * hop + n_fft] += w2
+        wss = wss[n_fft // 2:n_fft // 2 + hop * (T - 1)]
+        tiny = torch.finfo(torch.float32).tiny
+        inv = torch.where(wss > tiny, 1.0 / wss.clamp_min(tiny), torch.zeros_like(wss))
+        _WSS_CACHE[key] = inv.float().to(device)
+    return _WSS_CACHE[key]
+
+
+class _ISTFTFunction(torch.autograd.Function):
+    """y = istft(X). The iSTFT is linear; its adjoint is a scaled STFT: with
+    h = g / wss on the kept samples (zeros in the trimmed margins, i.e. center padding with
+    constants), dL/dX[k, f] = (c_f / n_fft) * rfft(w * h[k*hop : k*hop + n_fft])[f],
+    c_f = 1 at f = 0 and n_fft/2, else 2 (irfft's Hermitian weights). Both directions are
+    the fft.hip kernels (mst_istft_f32 / mst_stft_complex_f32)."""
+
+    @staticmethod
+    def forward(ctx, X, hop):
+        ctx.hop, ctx.T, ctx.F = hop, X.shape[1], X.shape[2]
+        return istft(X, hop)
+
+    @staticmethod
+    def backward(ctx, g):
+        n_fft = 2 * (ctx.F - 1)
+        h = (g.contiguous() * _inv_wss(ctx.T, ctx.hop, n_fft, g.device)).contiguous()
+        G = stft_complex(h, hop=ctx.hop, n_fft=n_fft, pad_mode="constant")
+        c = torch.full((ctx.F,), 2.0 / n_fft, device=g.device)
+        c[0] = c[-1] = 1.0 / n_fft
+        return G * c, None
+
+
+def istft_autograd(X, hop=256):
+    """Differentiable istft: (B, T, F) complex frame-major -> (B, hop*(T-1))."""
+    single = X.dim() == 2
+    Xb = (X.unsqueeze(0) if single else X).contiguous()
+    if not Xb.is_cuda:
+        raise RuntimeError("istft_autograd needs a CUDA tensor")
+    y = _ISTFTFunction.apply(Xb, int(hop))
+    return y[0] if single else y
+
+
+class _LogpowToMag(torch.autograd.Function):
+    """M = sqrt(expm1(clip(S, 0, 20))) (inference.py:109); dM/dS = e^S / (2M) inside (0, 20)."""
+
+    @staticmethod
+    def forward(ctx, S):
+        M = torch.expm1(S.clamp(0, 20)).sqrt()
+        ctx.save_for_backward(S, M)
+        return M
+
+    @staticmethod
+    def backward(ctx, g):
+        S, M = ctx.saved_tensors
+        inside = (S > 0) & (S < 20)
+        d = torch.where(inside, torch.exp(S.clamp(0, 20)) / (2 * M.clamp_min(1e-30)),
+                        torch.zeros_like(S))
+        return g * d
+
+
+def spectrogram_mss_loss(S_pred, target_audio, phase=None, hop=256, alpha=1.0, eps=1e-7,
+                         sizes=None):
+    """The README's intended loss (README.md:23) as a training loss on the
+    model's log-power output: render audio y = istft(sqrt(expm1(clip(S_pred,0,20))) * phase)
+    and take the multi-scale spectral loss against the target waveform. `phase` (B, T, F)
+    unit complex defaults to the target's own STFT phase (held constant); gradients flow to
+    S_pred through the iSTFT adjoint. S_pred: (B, 1025, T); target_audio: (B, hop*(T-1))."""
+    B, F, T = S_pred.shape
+    if target_audio.shape != (B, hop * (T - 1)):
+        raise ValueError("target_audio must be (B, hop*(T-1))")
+    if phase is None:
+        with torch.no_grad():
+            Xt = stft_complex(target_audio.contiguous(), hop=hop, n_fft=2 * (F - 1))
+            phase = Xt / Xt.abs().clamp_min(1e-16)
+            phase = torch.where(Xt.abs() > 0, phase, torch.ones_like(phase))
+    M = _LogpowToMag.apply(S_pred)
+    X = M.transpose(1, 2) * phase
+    y = istft_autograd(X, hop)
+    return multiscale_spectral_loss(y, target_audio, alpha=alpha, eps=eps,
+                                    sizes=MSS_SIZES if sizes is None else sizes)
+
+
 # ------------------------------------------------------------------- mel
 def _hz_to_mel(f):
     f = np.asarray(f, dtype=np.float64)
@@ -250,4 +342,5 @@ def spectral_convergence(S, y, hop=256):
 
 __all__ = ["stft_logpow", "stft_power", "stft_complex", "istft", "melspectrogram", "mel_basis",
            "griffinlim", "random_angles", "spectral_convergence", "n_frames",
-           "multiscale_spectral_loss", "MSS_SIZES", "math"]
+           "multiscale_spectral_loss", "MSS_SIZES", "math", "istft_autograd",
+           "spectrogram_mss_loss"]
