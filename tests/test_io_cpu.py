@@ -213,3 +213,19 @@ def test_device_loader_reproduces_dataloader(tmp_path):
         for r, g in zip(ref, got):
             for a, b in zip(r, g):
                 assert torch.equal(a, b)
+
+
+def test_musicnet_solo_piano_filter(tmp_path):
+    """extract_piano_pieces_from_musicnet_dataset.py:10-24: keep label files whose only
+    instrument is 1 (piano)."""
+    from ml_music_style_transfer_amd import musicnet
+    d = tmp_path / "test_labels"
+    d.mkdir()
+    rows = {"1759": [1, 1, 1], "2106": [1, 41, 1], "1819": [7, 7], "2303": [1]}
+    for k, inst in rows.items():
+        lines = ["start_time,end_time,instrument,note,start_beat,end_beat,note_value"]
+        lines += ["%d,%d,%d,60,0.0,1.0,Quarter" % (i * 10, i * 10 + 5, v) for i, v in enumerate(inst)]
+        (d / f"{k}.csv").write_text("\n".join(lines) + "\n")
+    got = musicnet.main(str(tmp_path), "test", str(tmp_path / "piano_pieces"))
+    assert sorted(got) == ["1759.csv", "2303.csv"]
+    assert (tmp_path / "piano_pieces_test.txt").read_text().split() == got
