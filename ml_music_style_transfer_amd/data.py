@@ -13,7 +13,9 @@ MI355X layout of the same data: the whole split is uploaded once as float32
 T=860 are ~30 GB, a tenth of one GPU's HBM) and each batch is three device gathers driven by
 2 x B indices. It reproduces `DataLoader(Dataseth5py(...), batch_size, shuffle)` batch for
 batch: the same RandomSampler permutation from torch's global generator and the same
-per-item `random` draws, in the same order.
+per-item `random` draws, in the same order. With `sampler=DistributedSampler(dataset, W, r)`
+each data-parallel rank keeps only its shard's batches (the split is still resident on every
+GPU: one upload, no per-step host traffic), as DataLoader(..., sampler=...) would give.
 """
 import random
 
@@ -72,10 +74,11 @@ def Process_Data(data_dir, n_train_read=None, n_test_read=None, batch_size=16, d
 class DeviceLoader:
     """DataLoader(dataset, batch_size, shuffle) over a Dataseth5py whose arrays live in HBM."""
 
-    def __init__(self, dataset, batch_size=16, shuffle=False, device="cuda"):
+    def __init__(self, dataset, batch_size=16, shuffle=False, device="cuda", sampler=None):
         self.dataset = dataset
         self.batch_size = batch_size
         self.shuffle = shuffle
+        self.sampler = sampler  # e.g. torch DistributedSampler: one rank's shard per process
         self.device = torch.device(device)
         ds = dataset
         self.n = ds.n_data
@@ -88,14 +91,22 @@ class DeviceLoader:
             self.S[i].copy_(torch.from_numpy(ds.specs[s].astype(np.float32)))
 
     def __len__(self):
-        return (self.n + self.batch_size - 1) // self.batch_size
+        n = len(self.sampler) if self.sampler is not None else self.n
+        return (n + self.batch_size - 1) // self.batch_size
+
+    def set_epoch(self, epoch):
+        if self.sampler is not None and hasattr(self.sampler, "set_epoch"):
+            self.sampler.set_epoch(epoch)
 
     def _order(self):
+        # torch.utils.data: every iterator draws its base seed from the global generator, then
+        # a RandomSampler draws its own seed from it; the permutation comes from a generator
+        # seeded with that. A given sampler (DistributedSampler) supplies the order itself.
+        torch.empty((), dtype=torch.int64).random_()
+        if self.sampler is not None:
+            return list(iter(self.sampler))
         if not self.shuffle:
             return list(range(self.n))
-        # torch.utils.data: the iterator draws its base seed, then RandomSampler its own seed,
-        # both from the global generator; the permutation comes from a generator seeded with it
-        torch.empty((), dtype=torch.int64).random_()
         seed = int(torch.empty((), dtype=torch.int64).random_().item())
         g = torch.Generator()
         g.manual_seed(seed)
@@ -103,7 +114,7 @@ class DeviceLoader:
 
     def __iter__(self):
         order = self._order()
-        for b0 in range(0, self.n, self.batch_size):
+        for b0 in range(0, len(order), self.batch_size):
             idx = order[b0:b0 + self.batch_size]
             sty, rnd = [], []
             for _ in idx:  # the per-item draws of Dataseth5py.__getitem__, in order
