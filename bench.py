@@ -127,12 +127,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if os.environ.get("MST_BENCH_BACKEND", "nccl") != "nccl":
+        local_rank %= torch.cuda.device_count()  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        # MST_BENCH_BACKEND=gloo rehearses the N>1 path with ranks sharing one GPU (RCCL needs
+        # one GPU per rank); measured runs use nccl (= RCCL over xGMI)
+        backend = os.environ.get("MST_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from ml_music_style_transfer_amd import dp, spectral
     from ml_music_style_transfer_amd import engine as E
@@ -160,6 +168,8 @@ def main():
     ref_audio = torch.from_numpy(ref_audio).to(dev)
     data = torch.from_numpy(np.concatenate([roll, onoff], 1)).to(dev)  # (B, 256, T) train.py:84-85
 
+    comm_on = [True]  # off only for the exposed-communication leg after the timed region
+
     def step():
         opt.zero_grad()
         target = spectral.stft_logpow(tgt_audio, hop=HOP)           # (B, 1025, 252)
@@ -168,7 +178,7 @@ def main():
         y = model(split[0], x_audio, split[1])
         loss = E.l1_loss(y, target)
         loss.backward()               # overlapped bucket all-reduces start inside backward
-        if world > 1 and args.no_overlap:
+        if world > 1 and args.no_overlap and comm_on[0]:
             dp.allreduce_gradients(model)
         opt.step()                    # waits for the all-reduce, then the update (or joins it)
         return loss
@@ -223,6 +233,13 @@ def main():
         a[1] += f
         a[2] += 1
 
+    comm = None
+    if world > 1:
+        try:
+            comm = all_reduce_leg(model, step, comm_on, world, dev, ms_per_step, args)
+        except Exception as e:  # a report leg must not cost the measured line
+            comm = {"error": repr(e)[:200]}
+
     out = {
         "metric": "training-step spectrogram-frames/sec, batch 32, 4 s @ 16 kHz, 1/2/4/8 GPUs",
         "value": round(value, 1),
@@ -260,6 +277,8 @@ def main():
         },
         "final_loss": round(final_loss, 5),
     }
+    if comm is not None:
+        out["allreduce"] = comm
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if world > 1:
@@ -267,6 +286,48 @@ def main():
         torch.distributed.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def _timed_max(fn, reps, dev):
+    """Wall time of `reps` calls between barrier + synchronize brackets, max over ranks."""
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    torch.cuda.synchronize()
+    tt = torch.tensor([time.perf_counter() - t0], device=dev)
+    torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+    return tt.item()
+
+
+def all_reduce_leg(model, step, comm_on, world, dev, ms_per_step, args):
+    """SURVEY 8(d) config 4, measured after the timed region (the weights diverge here, nothing
+    after it trains): (1) the same step with the gradient exchange switched off, so exposed
+    communication = ms_per_step - compute-only ms; (2) the bucketed gradient all-reduce alone,
+    bus bandwidth = 2 (N-1)/N x bytes / time (RCCL's busbw convention)."""
+    from ml_music_style_transfer_amd import dp
+    saved = getattr(model, "_mst_dp", None)
+    model._mst_dp, comm_on[0] = None, False
+    step()
+    k = max(2, min(args.steps, 5))
+    compute_ms = 1000.0 * _timed_max(step, k, dev) / k
+    model._mst_dp, comm_on[0] = saved, True
+    _, _, n = model.flat_buffers()
+    nbytes = 4 * n
+    dp.allreduce_gradients(model, bucket_bytes=dp.OVERLAP_BUCKET_BYTES)
+    reps = 3
+    t_ar = _timed_max(lambda: dp.allreduce_gradients(model, bucket_bytes=dp.OVERLAP_BUCKET_BYTES),
+                      reps, dev) / reps
+    return {"grad_bytes": nbytes, "bucket_bytes": dp.OVERLAP_BUCKET_BYTES,
+            "allreduce_ms": round(1000.0 * t_ar, 3),
+            "bus_GBps": round(2.0 * (world - 1) / world * nbytes / t_ar / 1e9, 1),
+            "compute_only_ms_per_step": round(compute_ms, 3),
+            "exposed_comm_ms_per_step": round(ms_per_step - compute_ms, 3),
+            "overlapped": not args.no_overlap}
 
 
 if __name__ == "__main__":
