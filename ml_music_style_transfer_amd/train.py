@@ -299,6 +299,7 @@ def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2):
             print('Train Epoch: {} [{}/{} ({:.0f}%)]\t Loss: {:.6f}'.format(
                 epoch, batch_idx * len(data), len(train_loader.dataset),
                 100. * batch_idx / len(train_loader), loss.item() / len(data)))
+    train_loss = _sum_over_ranks(train_loss)  # data parallel: every rank's batches
     print('====> Epoch: {} Average loss: {:.4f}'.format(epoch, train_loss / len(train_loader.dataset)))
     return train_loss / len(train_loader.dataset)
 
@@ -314,6 +315,7 @@ def test(model, epoch, test_loader, scheduler, iter_test_loss):
             loss = E.mse_loss(y_pred, _cuda(target))
             iter_test_loss.append(loss.item())
             test_loss += loss
+        test_loss = _sum_over_ranks(test_loss)  # one scheduler decision on every rank
         test_loss /= len(test_loader.dataset)
         scheduler.step(test_loss)
         print('====> Test set loss: {:.4f}'.format(test_loss))
@@ -340,24 +342,64 @@ class SyntheticSpectrogramDataset(torch.utils.data.Dataset):
         return self.n
 
 
-def main(args):
+def _init_data_parallel():
+    """One process per GPU under torch.distributed.run (WORLD_SIZE > 1): backend nccl (= RCCL
+    over xGMI), or $MST_DIST_BACKEND (gloo: ranks may share a GPU, for rehearsal/tests)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1
+    import torch.distributed as dist
+    backend = os.environ.get("MST_DIST_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend)
+    return dist.get_rank(), dist.get_world_size()
+
+
+def _sum_over_ranks(t):
+    if dp.is_dist() and isinstance(t, torch.Tensor):
+        import torch.distributed as dist
+        t = t.detach().clone()
+        dist.all_reduce(t)
+    return t
+
+
+def main(args, return_model=False):
     """train.py:173-208. Reads `<data_dir>_train.hdf5` / `_test.hdf5` (data.Process_Data,
     HBM-resident loaders) when they exist, else a synthetic dataset of the same layout."""
     hp = hyperparams(args)
+    rank, world = _init_data_parallel()
     exp_root = os.path.join(os.path.abspath('./'), 'experiments')
     os.makedirs(exp_root, exist_ok=True)
     exp_dir = os.path.join(exp_root, hp.exp_name)
     os.makedirs(exp_dir, exist_ok=True)
     model = PerformanceNet().cuda()
+    if world > 1:
+        dp.broadcast_parameters(model)         # every rank starts from rank 0's weights
+        dp.enable_overlapped_allreduce(model)  # bucket all-reduces inside backward
+        model._seed = rank << 24               # per-rank dropout streams
     optimizer = make_optimizer(model, lr=1e-3)
     model.zero_grad()
     optimizer.zero_grad()
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, 'min')
     if args.data_dir and os.path.exists(args.data_dir + '_train.hdf5'):
-        from .data import Process_Data
+        from .data import DeviceLoader, Process_Data
         train_loader, test_loader = Process_Data(args.data_dir, n_train_read=args.n_train_read,
                                                  n_test_read=args.n_test_read,
                                                  batch_size=args.batch_size)
+        if world > 1:  # one shard of every epoch per rank, per-rank style/cond draws
+            from torch.utils.data.distributed import DistributedSampler
+            import random
+            random.seed(42 + rank)
+            tr, te = train_loader.dataset, test_loader.dataset
+            train_loader = DeviceLoader(tr, args.batch_size, sampler=DistributedSampler(
+                tr, num_replicas=world, rank=rank, shuffle=True))
+            test_loader = DeviceLoader(te, args.batch_size, sampler=DistributedSampler(
+                te, num_replicas=world, rank=rank, shuffle=False))
     else:
         T = args.frames
         train_ds = SyntheticSpectrogramDataset(args.n_train_read or 32, T=T, seed=1)
@@ -367,21 +409,25 @@ def main(args):
         test_loader = torch.utils.data.DataLoader(test_ds, batch_size=args.batch_size)
     print('start training')
     for epoch in range(hp.train_epoch):
+        if hasattr(train_loader, "set_epoch"):
+            train_loader.set_epoch(epoch)
         loss = train(model, epoch, train_loader, optimizer, hp.iter_train_loss)
         hp.loss_history.append(loss.item())
         if epoch % hp.test_freq == 0:
             test_loss = test(model, epoch, test_loader, scheduler, hp.iter_test_loss)
             hp.test_loss_history.append(test_loss.item())
             if test_loss < hp.best_loss:
+                hp.best_loss = test_loss.item()
+                hp.best_epoch = epoch + 1
+                if rank != 0:
+                    continue
                 print("saving model")
                 torch.save({'epoch': epoch + 1, 'state_dict': model.state_dict(),
                             'optimizer': optimizer.state_dict()},
                            os.path.join(exp_dir, 'checkpoint-{}.tar'.format(str(epoch + 1))))
-                hp.best_loss = test_loss.item()
-                hp.best_epoch = epoch + 1
                 with open(os.path.join(exp_dir, 'hyperparams.json'), 'w') as outfile:
                     json.dump(hp.__dict__, outfile)
-    return hp
+    return (hp, model) if return_model else hp
 
 
 def parse_args(argv=None):

@@ -93,3 +93,66 @@ def test_overlapped_allreduce_two_ranks_one_gpu(cuda):
         local, reduced, issued, nb = res[r]
         assert nb > 10 and issued == nb  # every bucket was issued by the end of backward
         torch.testing.assert_close(reduced, mean, rtol=1e-5, atol=1e-9)
+
+
+def _train_worker(rank, world, port, workdir, q):
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(280, exit=True, file=sys.stderr)
+    os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "RANK": str(rank),
+                       "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "MST_DIST_BACKEND": "gloo"})
+    os.chdir(workdir)
+    from ml_music_style_transfer_amd import train as TR
+    hp, model = TR.main(TR.parse_args(["-data-dir", os.path.join(workdir, "piano"), "-epochs",
+                                       "2", "--batch-size", "2"]), return_model=True)
+    flat, _, n = model.flat_buffers()
+    idx = torch.randint(0, n, (NSAMP,), generator=torch.Generator().manual_seed(4)).to(flat.device)
+    torch.cuda.synchronize()
+    q.put((rank, hp.loss_history, hp.test_loss_history, hp.best_epoch, flat[idx].cpu()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_train_main_data_parallel_two_ranks(cuda, tmp_path, monkeypatch):
+    """train.main under WORLD_SIZE=2 (train.py:173-208 + SURVEY §8(e)): rank 0's weights
+    broadcast, DistributedSampler shards of the HBM-resident HDF5 split, overlapped gradient
+    all-reduce, loss sums over ranks, checkpoint from rank 0 only. After two epochs both
+    ranks hold identical weights and report identical epoch losses."""
+    import numpy as np
+    from ml_music_style_transfer_amd import data, train as TR
+    rng = np.random.default_rng(8)
+    for split, N in (("train", 8), ("test", 4)):
+        T = 44
+        pr = (rng.random((N, T, 128)) < 0.1).astype(float)
+        oo = np.diff(np.concatenate([np.zeros((N, 1, 128)), pr], 1), axis=1)
+        data.write_split(str(tmp_path / ("piano_%s.hdf5" % split)), pr, oo,
+                         {"cuba": 2 * rng.random((N, 1025, T)), "upright": 2 * rng.random((N, 1025, T))})
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, str(tmp_path), q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    deadline = time.monotonic() + 300
+    while len(res) < world:
+        try:
+            r, lh, th, be, pr_ = q.get(timeout=5)
+            res[r] = (lh, th, be, pr_)
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.monotonic() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"worker failed (exit codes {dead})")
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1] and res[0][2] == res[1][2]
+    assert all(np.isfinite(res[0][0])) and len(res[0][0]) == 2
+    torch.testing.assert_close(res[0][3], res[1][3], rtol=0, atol=0)
+    exp = tmp_path / "experiments" / "piano_test"
+    assert (exp / ("checkpoint-%d.tar" % res[0][2])).exists() and (exp / "hyperparams.json").exists()
