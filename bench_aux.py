@@ -99,6 +99,39 @@ def _line(metric, value, unit, world, steps, warmup, ms, config, roofline, cpu, 
     return out
 
 
+def _cpu_front(job):
+    """One clip through the oracle (runs in a spawned worker: NumPy only, no GPU)."""
+    from oracle import spectral_ref as SR
+    name, clip = job
+    return (SR.logpow(clip, 2048, bench.HOP) if name == "logpow"
+            else SR.melspec(clip, bench.SR, 2048, bench.HOP)).shape
+
+
+def _cpu_parallel_rate(name, clips):
+    """NumPy's FFT is single-threaded, so the n-way CPU number is a process pool
+    (spawned workers, no GPU state) over the clips; pool start-up is outside the timing."""
+    import multiprocessing as mp
+    procs = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
+    saved = {k: os.environ.get(k) for k in keys}
+    os.environ.update({k: "1" for k in keys})  # one BLAS thread per worker: no oversubscription
+    try:
+        pool = mp.get_context("spawn").Pool(procs)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with pool:
+        pool.map(_cpu_front, [(name, clips[0])] * procs)  # warm every worker
+        t0 = time.perf_counter()
+        pool.map(_cpu_front, [(name, c) for c in clips], chunksize=max(1, len(clips) // (4 * procs)))
+        dt = time.perf_counter() - t0
+    return {"value": round(len(clips) / dt, 2), "cores": procs,
+            "sample": f"{len(clips)} clips, multiprocessing pool of {procs} spawned workers"}
+
+
 def frontend(args, world, rank, dev):
     from ml_music_style_transfer_amd import spectral
     from oracle import spectral_ref as SR
@@ -124,6 +157,10 @@ def frontend(args, world, rank, dev):
             c = (time.perf_counter() - t0) / n
             cpu = {"value": round(1.0 / c, 2), "unit": "clips/s", "cores": 1, "kind": "port",
                    "sample": f"{n} clips through oracle/spectral_ref.py (NumPy pocketfft float64, 1 thread)"}
+            try:
+                cpu["parallel"] = _cpu_parallel_rate(name, list(x[:min(B, 256)]))
+            except Exception as e:  # a baseline leg must not cost the measured line
+                cpu["parallel"] = {"error": repr(e)[:200]}
         res.append(_line(f"STFT {name} clips/s, 256 x 4 s @ 16 kHz", world * B / dt, "clips/s", world,
                          args.steps, args.warmup, dt * 1e3,
                          {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,
