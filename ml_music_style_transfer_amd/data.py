@@ -83,6 +83,11 @@ class DeviceLoader:
         ds = dataset
         self.n = ds.n_data
         self.styles = list(ds.styles)
+        short = [s for s in self.styles if ds.specs[s].shape[0] != self.n]
+        if short or not self.styles:
+            # get_data skips a style whose audio is missing for a song, so its rows no longer
+            # line up with pianoroll[i]; the reference then fails (or mismatches) per item
+            raise ValueError(f"spec datasets {short or self.styles} do not have {self.n} rows")
         x = np.concatenate((ds.pianoroll, ds.onoff), axis=-1).astype(np.float32)
         self.X = torch.from_numpy(x).to(self.device).transpose(1, 2).contiguous()
         self.S = torch.empty((len(self.styles), self.n) + tuple(ds.specs[self.styles[0]].shape[1:]),

@@ -147,7 +147,10 @@ class MidiFile:
         while i + 8 <= len(data) and len(tracks) < ntrk:
             cid, ln = data[i:i + 4], struct.unpack(">I", data[i + 4:i + 8])[0]
             if cid == b"MTrk":
-                tracks.append(_parse_track(data[i + 8:i + 8 + ln]))
+                try:
+                    tracks.append(_parse_track(data[i + 8:i + 8 + ln]))
+                except IndexError:
+                    raise ValueError("truncated MTrk chunk") from None
             i += 8 + ln
         if not tracks:
             raise ValueError("no MTrk chunks")

@@ -40,6 +40,8 @@ def _read_raw(path):
     if fmt is None or body is None:
         raise ValueError("WAV without fmt/data chunk: %s" % path)
     tag, nch, sr, _, _, bits = fmt
+    if (tag == 3 and bits not in (32, 64)) or (tag == 1 and bits not in (8, 16, 24, 32)):
+        raise ValueError("unsupported WAV sample width: %d bits (format %d)" % (bits, tag))
     if tag == 3:
         x = np.frombuffer(body, dtype={32: "<f4", 64: "<f8"}[bits]).astype(np.float64)
     elif tag == 1:

@@ -268,3 +268,15 @@ def test_device_loader_distributed_shards(tmp_path):
         s2.set_epoch(0)
         seen += list(iter(s2))
     assert sorted(set(seen)) == list(range(10))
+
+
+def test_malformed_inputs_raise_valueerror(tmp_path):
+    hdr = b"MThd" + struct.pack(">IHHH", 6, 0, 1, 480)
+    with pytest.raises(ValueError):
+        midi.MidiFile(hdr + b"MTrk" + struct.pack(">I", 3) + b"\x00\x90\x3c")  # cut mid-event
+    fmt = struct.pack("<HHIIHH", 1, 1, 44100, 44100 * 2, 2, 12)
+    wav = b"RIFF" + struct.pack("<I", 36) + b"WAVE" + b"fmt " + struct.pack("<I", 16) + fmt + \
+        b"data" + struct.pack("<I", 0)
+    (tmp_path / "c.wav").write_bytes(wav)
+    with pytest.raises(ValueError):
+        wavio.load(str(tmp_path / "c.wav"))
