@@ -73,9 +73,22 @@ def piano_rolls(notes_all, T=T_FRAMES, wps=SR // HOP):
     return rolls, rolls - prev
 
 
-def cpu_baseline(B=4, steps=2):
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo) for the baseline's record."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(B=32, steps=1):
     """The oracle's torch-CPU restatement of the reference training step (oracle/model_ref.py),
-    timed on this host: bounded sample of B clips x T=252, `steps` timed steps after 1 warmup."""
+    timed on this host at the benchmarked configuration (B=32, T=252): `steps` timed steps after
+    one untimed warm-up step (fwd + L1 + bwd + Adam, dropout on)."""
     from oracle import model_ref as R
     from oracle import detinit
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -102,9 +115,45 @@ def cpu_baseline(B=4, steps=2):
         step(i + 1)
     dt = (time.perf_counter() - t0) / steps
     return {"value": round(B * T_FRAMES / dt, 2), "unit": "spectrogram-frames/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{steps} timed train steps (fwd+L1+bwd+Adam) of oracle/model_ref.py on "
-                      f"torch-CPU, B={B}, T={T_FRAMES}, {threads} threads ({dt:.2f} s/step)"}
+            "kind": "port", "cpu_model": cpu_model(),
+            "sample": f"{steps} timed train step(s) (fwd+L1+bwd+Adam, dropout on) of "
+                      f"oracle/model_ref.py on torch-CPU after 1 warm-up step, B={B}, T={T_FRAMES} "
+                      f"(the benchmarked configuration), {threads} threads ({dt:.2f} s/step)"}
+
+
+def gemm_traffic():
+    """HBM-side bytes per gemm_kernel launch from this round's PMC passes (tools/pmc_traffic.py
+    over `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of this bench), newest round
+    first. Returns (bytes or None, source note)."""
+    pdir = os.path.join(ROOT, "profiles")
+    rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) \
+        if os.path.isdir(pdir) else []
+    for r in rounds:
+        tj = os.path.join(pdir, r, "gemm_traffic.json")
+        if os.path.exists(tj):
+            with open(tj) as fh:
+                d = json.load(fh)
+            return round(d["traffic_bytes_per_launch"]), (
+                f"profiles/{r}/gemm_traffic.json ({d.get('build', 'build not recorded')}): "
+                "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes over this bench, "
+                "2 x fetch + write per gemm_kernel launch")
+    return None, None
+
+
+def aux_legs(world, rank, dev, cpu):
+    """BASELINE configs[1] (STFT/mel + 60-iteration Griffin-Lim, 256 x 4 s @ 16 kHz) and
+    configs[4] (multi-scale spectral loss, 10 s @ 22.05 kHz) timed in the same run as the
+    training step (bench_aux.py's legs, shortened; one-thread oracle CPU baselines)."""
+    import bench_aux
+    a = argparse.Namespace(steps=10, warmup=2, clips=256, pairs=32, no_cpu_baseline=not cpu,
+                           parallel_cpu=False)
+    out = {}
+    for fn in (bench_aux.frontend, bench_aux.griffinlim, bench_aux.mss):
+        for ln in fn(a, world, rank, dev):
+            key = ln["config"]["workload"]
+            out[key] = {k: ln[k] for k in ("metric", "value", "unit", "ms_per_step", "kernel_ms",
+                                           "roofline", "cpu_baseline") if k in ln}
+    return out
 
 
 def main():
@@ -115,6 +164,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-timing-steps", type=int, default=2)
+    ap.add_argument("--no-aux", action="store_true",
+                    help="skip the config-2 / config-5 legs (STFT, mel, Griffin-Lim, multi-scale loss)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="all-reduce after backward instead of overlapped bucket all-reduces")
     ap.add_argument("--adam-overlap", action="store_true",
@@ -152,6 +203,7 @@ def main():
     torch.manual_seed(1234)
     model = PerformanceNet().to(dev)
     model.train()
+    model._seed += rank << 24  # per-rank dropout streams (train.main does the same)
     dp.broadcast_parameters(model)
     if world > 1 and not args.no_overlap:
         dp.enable_overlapped_allreduce(model)
@@ -204,6 +256,8 @@ def main():
     ms_per_step = 1000.0 * dt / args.steps
     value = world * B * T_FRAMES / (dt / args.steps)
     final_loss = loss.item()
+    if not math.isfinite(final_loss):
+        raise SystemExit(f"non-finite training loss {final_loss}: the measured step is broken")
 
     # roofline leg: per-launch HIP events around every GEMM (fp32 MFMA implicit GEMM) of a few
     # extra steps, on the launch stream; achieved = algorithmic FLOPs / summed kernel time.
@@ -219,13 +273,7 @@ def main():
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     # algorithmic bytes per GEMM launch: each operand and the output once, (MK + KN + MN) x 4
     alg_bytes = [4.0 * (shp[0] * shp[2] + shp[2] * shp[1] + shp[0] * shp[1]) for *_, shp in log if shp]
-    traffic, traffic_src = None, None
-    tj = os.path.join(ROOT, "profiles", "r01", "gemm_traffic.json")
-    if os.path.exists(tj):
-        with open(tj) as fh:
-            traffic = round(json.load(fh)["traffic_bytes_per_launch"])
-        traffic_src = ("profiles/r01/gemm_traffic.json: rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE "
-                       "passes over this bench, 2 x fetch + write per gemm_kernel launch")
+    traffic, traffic_src = gemm_traffic()
     by_tag = {}
     for s, e, f, tag, _ in log:
         a = by_tag.setdefault(tag, [0.0, 0.0, 0])
@@ -279,6 +327,8 @@ def main():
     }
     if comm is not None:
         out["allreduce"] = comm
+    if not args.no_aux:
+        out["aux"] = aux_legs(world, rank, dev, cpu=not args.no_cpu_baseline)
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if world > 1:

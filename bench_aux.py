@@ -35,15 +35,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
 def _dist():
+    """One process per GPU under torch.distributed.run; every rank takes its own clips (seeded by
+    rank, no collective on the data path), barriers + a MAX of the wall time bracket the timing.
+    MST_BENCH_BACKEND=gloo rehearses it with ranks sharing one GPU (not an xGMI measurement)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MST_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     return world, rank, dev
 
 
@@ -63,7 +72,7 @@ def _timed(fn, steps, warmup, world):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([dt], device="cuda")
+        tt = torch.tensor([dt], device=torch.cuda.current_device())
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         dt = tt.item()
     return dt / steps
@@ -157,10 +166,11 @@ def frontend(args, world, rank, dev):
             c = (time.perf_counter() - t0) / n
             cpu = {"value": round(1.0 / c, 2), "unit": "clips/s", "cores": 1, "kind": "port",
                    "sample": f"{n} clips through oracle/spectral_ref.py (NumPy pocketfft float64, 1 thread)"}
-            try:
-                cpu["parallel"] = _cpu_parallel_rate(name, list(x[:min(B, 256)]))
-            except Exception as e:  # a baseline leg must not cost the measured line
-                cpu["parallel"] = {"error": repr(e)[:200]}
+            if getattr(args, "parallel_cpu", True):
+                try:
+                    cpu["parallel"] = _cpu_parallel_rate(name, list(x[:min(B, 256)]))
+                except Exception as e:  # a baseline leg must not cost the measured line
+                    cpu["parallel"] = {"error": repr(e)[:200]}
         res.append(_line(f"STFT {name} clips/s, 256 x 4 s @ 16 kHz", world * B / dt, "clips/s", world,
                          args.steps, args.warmup, dt * 1e3,
                          {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,

@@ -23,8 +23,8 @@
  *   mst_conv_wgrad_f32       weight gradients of the same layers (loss.backward(), train.py:140)
  *   mst_instnorm_lrelu_fwd_f32 / _bwd_f32
  *                            model/model.py:40-53,65-69,81-89   InstanceNorm1d + LeakyReLU(0.01) [+ MaxPool1d(2)]
- *   mst_l1_lrelu_fwd_f32 / _bwd_f32
- *                            model/model.py:299 + model/train.py:132-135,140  lrelu(lastconv) + nn.L1Loss
+ *   mst_l1_fwd_f32 / _bwd_f32, mst_mse_fwd_f32
+ *                            model/train.py:132-135,140,158     nn.L1Loss fwd/bwd, nn.MSELoss (test)
  *   mst_adam_f32 / _ex_f32   model/train.py:188,143             optim.Adam(lr=1e-3)
  *   mst_onoff_f32            preprocessing/preprocess.py:148-155 piano-roll binarise + onset/offset
  */
@@ -148,14 +148,9 @@ int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float sc
 int mst_bias_grad_rows_f32(const float* rowsum, int32_t B, int32_t C, float scale, float* db,
                            int32_t accumulate, void* stream);
 
-/* ---- lastconv LeakyReLU + L1 loss (model.py:299, train.py:132-135) ----
- * fwd: y = lrelu(ypre) written to y (nullable); loss_partials[nblocks] (double) then
- *      loss[0] = sum|y - target| / n. bwd: dypre = gscale[0] * sign(y - t)/n * lrelu'(ypre). */
+/* ---- L1 / MSE loss (train.py:132-135,158): loss[0] = sum|pred - target| / n (or squared),
+ * accumulated as double partials in a workspace of mst_l1_workspace_size(n) bytes. ---- */
 size_t mst_l1_workspace_size(int64_t n);
-int mst_l1_lrelu_fwd_f32(const float* ypre, const float* target, int64_t n, float slope, float* y,
-                         float* loss, void* workspace, void* stream);
-int mst_l1_lrelu_bwd_f32(const float* ypre, const float* target, int64_t n, float slope,
-                         const float* gscale, float* dypre, void* stream);
 int mst_l1_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* workspace,
                    void* stream);
 int mst_mse_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* workspace,
@@ -173,19 +168,20 @@ int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, fl
                           void* stream);
 
 /* ---- Adam over a flat parameter buffer (torch.optim.Adam semantics, no weight decay) ----
- * lr_step = lr / (1 - b1^t); inv_bc2_sqrt = 1/sqrt(1 - b2^t). */
+ * At step t (1-based): lr_step = lr / (1 - b1^t); bc2_sqrt = sqrt(1 - b2^t) (NOT its inverse):
+ *   m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2;  p -= lr_step * m / (sqrt(v) / bc2_sqrt + eps).
+ * p, g, m, v: n floats each, 16-byte aligned, the same element order (any layout, shared). */
 int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
-                 float b2, float eps, float inv_bc2_sqrt, void* stream);
+                 float b2, float eps, float bc2_sqrt, void* stream);
 /* The same update over at most max_blocks 256-thread workgroups (grid-stride): a background
  * launch beside other kernels (one workgroup per CU leaves the GEMMs their occupancy). */
 int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
-                    float b1, float b2, float eps, float inv_bc2_sqrt, int32_t max_blocks,
+                    float b1, float b2, float eps, float bc2_sqrt, int32_t max_blocks,
                     void* stream);
 
 /* ---- elementwise helpers ---- */
 int mst_scale_f32(float* x, int64_t n, float s, void* stream);
 int mst_fill_f32(float* x, int64_t n, float v, void* stream);
-int mst_axpby_f32(const float* x, float* y, int64_t n, float a, float b, void* stream); /* y = a x + b y */
 
 /* ---- front end: STFT (Hann periodic, center, pad_mode), one clip per row of x (B, L) ----
  * n_fft == 2048 and hop in {64..1024} supported by the LDS FFT; T = 1 + L/hop, F = n_fft/2 + 1.

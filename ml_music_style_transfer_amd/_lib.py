@@ -68,10 +68,6 @@ SIGNATURES = {
     "mst_bias_grad_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_float, c_void_p, c_int32,
                                     c_void_p]),
     "mst_l1_workspace_size": (c_size_t, [c_int64]),
-    "mst_l1_lrelu_fwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p,
-                                       c_void_p, c_void_p]),
-    "mst_l1_lrelu_bwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p,
-                                       c_void_p]),
     "mst_l1_fwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "mst_mse_fwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "mst_l1_bwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
@@ -83,7 +79,6 @@ SIGNATURES = {
                                   c_float, c_float, c_float, c_float, c_int32, c_void_p]),
     "mst_scale_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
     "mst_fill_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
-    "mst_axpby_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p]),
     "mst_stft_logpow_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,
                                       c_void_p, c_void_p]),
     "mst_stft_power_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,

@@ -265,21 +265,14 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict_
 // ---------------------------------------------------------------------------
 // L1 / MSE loss: per-block double partials, then one block finishes (deterministic).
 // ---------------------------------------------------------------------------
-template <int MODE>  // 0: L1 of lrelu(pre) vs t (writes y), 1: L1(pred, t), 2: MSE(pred, t)
+template <int MODE>  // 1: L1(pred, t), 2: MSE(pred, t)
 __global__ __launch_bounds__(256) void loss_partial_kernel(const float* __restrict__ x,
                                                            const float* __restrict__ t,
-                                                           long long n, float slope,
-                                                           float* __restrict__ y,
-                                                           double* __restrict__ part) {
+                                                           long long n, double* __restrict__ part) {
   double s = 0.0;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (long long)gridDim.x * blockDim.x) {
-    float v = x[i];
-    if (MODE == 0) {
-      v = lrelu(v, slope);
-      if (y) y[i] = v;
-    }
-    float d = v - t[i];
+    float d = x[i] - t[i];
     s += (MODE == 2) ? (double)d * d : (double)fabsf(d);
   }
   __shared__ double red[4];
@@ -298,21 +291,6 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const double* __restric
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) loss[0] = (float)((red[0] + red[1] + red[2] + red[3]) / (double)n);
-}
-
-__global__ __launch_bounds__(256) void l1_lrelu_bwd_kernel(const float* __restrict__ pre,
-                                                           const float* __restrict__ t, long long n,
-                                                           float slope,
-                                                           const float* __restrict__ gscale,
-                                                           float* __restrict__ dpre) {
-  const float g = (gscale ? gscale[0] : 1.f) / (float)n;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float p = pre[i];
-    float d = lrelu(p, slope) - t[i];
-    float sg = d > 0.f ? g : (d < 0.f ? -g : 0.f);
-    dpre[i] = p > 0.f ? sg : sg * slope;
-  }
 }
 
 // Adam (torch.optim.Adam, single-tensor formulation): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g^2;
@@ -409,14 +387,6 @@ __global__ void relu_gate_bwd_kernel(const float* __restrict__ d, const float* _
     out[i] = h[i] > 0.f ? d[i] * s : 0.f;
 }
 
-// y = a * x + b * y
-__global__ void axpby_kernel(const float* __restrict__ x, float* __restrict__ y, long long n,
-                             float a, float b) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
-    y[i] = a * x[i] + b * y[i];
-}
-
 int grid_for(long long n, int per = 256, int cap = 8192) {
   long long g = (n + per - 1) / per;
   if (g > cap) g = cap;
@@ -478,41 +448,27 @@ int mst_bias_grad_rows_f32(const float* rowsum, int32_t B, int32_t C, float scal
 
 size_t mst_l1_workspace_size(int64_t n) { return (size_t)grid_for(n, 256 * 8, 1024) * sizeof(double); }
 
-static int loss_launch(int mode, const float* x, const float* t, int64_t n, float slope, float* y,
-                       float* loss, void* ws, void* stream) {
+static int loss_launch(int mode, const float* x, const float* t, int64_t n, float* loss, void* ws,
+                       void* stream) {
   MST_REQUIRE(x && t && loss && ws && n > 0);
   hipStream_t st = (hipStream_t)stream;
   int nb = grid_for(n, 256 * 8, 1024);
   double* part = (double*)ws;
-  if (mode == 0) hipLaunchKernelGGL(loss_partial_kernel<0>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
-  else if (mode == 1) hipLaunchKernelGGL(loss_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
-  else hipLaunchKernelGGL(loss_partial_kernel<2>, dim3(nb), dim3(256), 0, st, x, t, n, slope, y, part);
+  if (mode == 1) hipLaunchKernelGGL(loss_partial_kernel<1>, dim3(nb), dim3(256), 0, st, x, t, n, part);
+  else hipLaunchKernelGGL(loss_partial_kernel<2>, dim3(nb), dim3(256), 0, st, x, t, n, part);
   MST_CHECK_LAUNCH();
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part, nb, (long long)n, loss);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
 
-int mst_l1_lrelu_fwd_f32(const float* ypre, const float* target, int64_t n, float slope, float* y,
-                         float* loss, void* ws, void* stream) {
-  return loss_launch(0, ypre, target, n, slope, y, loss, ws, stream);
-}
 int mst_l1_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* ws,
                    void* stream) {
-  return loss_launch(1, pred, target, n, 0.f, nullptr, loss, ws, stream);
+  return loss_launch(1, pred, target, n, loss, ws, stream);
 }
 int mst_mse_fwd_f32(const float* pred, const float* target, int64_t n, float* loss, void* ws,
                     void* stream) {
-  return loss_launch(2, pred, target, n, 0.f, nullptr, loss, ws, stream);
-}
-
-int mst_l1_lrelu_bwd_f32(const float* ypre, const float* target, int64_t n, float slope,
-                         const float* gscale, float* dypre, void* stream) {
-  MST_REQUIRE(ypre && target && dypre && n > 0);
-  hipLaunchKernelGGL(l1_lrelu_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream,
-                     ypre, target, (long long)n, slope, gscale, dypre);
-  MST_CHECK_LAUNCH();
-  return MST_OK;
+  return loss_launch(2, pred, target, n, loss, ws, stream);
 }
 
 int mst_l1_bwd_f32(const float* pred, const float* target, int64_t n, const float* gscale, float* dx,
@@ -538,15 +494,6 @@ int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, fl
   MST_REQUIRE(d && h && out && n > 0);
   hipLaunchKernelGGL(relu_gate_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d,
                      h, (long long)n, s, out);
-  MST_CHECK_LAUNCH();
-  return MST_OK;
-}
-
-int mst_axpby_f32(const float* x, float* y, int64_t n, float a, float b, void* stream) {
-  MST_REQUIRE(x && y && n >= 0);
-  if (n == 0) return MST_OK;
-  hipLaunchKernelGGL(axpby_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y,
-                     (long long)n, a, b);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }

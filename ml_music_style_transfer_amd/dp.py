@@ -83,6 +83,13 @@ def flat_buckets(model, bucket_bytes):
     return buckets, bucket_of, count
 
 
+def native_avg():
+    """True when the backend averages inside the collective (ReduceOp.AVG: nccl = RCCL). Other
+    backends (gloo) SUM and each bucket is then scaled by 1/world on the stream that waits for
+    it, so both paths deliver an averaged bucket at the same point of the stream order."""
+    return dist.get_backend() == "nccl"
+
+
 class OverlappedAllReduce:
     """Gradient all-reduce overlapped with the backward pass.
 
@@ -93,10 +100,12 @@ class OverlappedAllReduce:
     all-reduce is issued from the compute stream (RCCL's stream waits for the gradient
     kernels already enqueued, later backward kernels keep running beside it). Buckets are
     issued strictly in order, so every rank issues the same collectives in the same order.
-    `finish()` (called by Adam.step or dp.finish_gradients) makes the compute stream wait.
 
-    Gradient accumulation stays correct: the part of a bucket accumulated in earlier
-    backward passes is identical on all ranks, so averaging the sum averages the new part.
+    `wait_bucket(b)` makes the current stream wait for bucket b's average (BackwardAdam calls it
+    on its side stream); `finish()` (Adam.step or dp.finish_gradients) does it for every bucket
+    on the compute stream. Gradient accumulation: a new backward pass first finishes the
+    previous pass's exchange, so the accumulated buffer holds avg(g1) + g2_local, identical on
+    every rank in its first part, and its average is avg(g1) + avg(g2).
     """
 
     def __init__(self, model, bucket_bytes=OVERLAP_BUCKET_BYTES):
@@ -105,20 +114,33 @@ class OverlappedAllReduce:
         self.buckets, self.bucket_of, self.count = flat_buckets(model, bucket_bytes)
         self.grad = grad
         self.works = []
+        self.scaled = []
         self.remaining = list(self.count)
         self.next = 0
         self.active = False
 
     def begin(self):
+        if self.active:
+            self.finish()
         self.remaining = list(self.count)
         self.next = 0
         self.works = []
+        self.scaled = []
         self.active = is_dist()
 
     def _launch(self, b):
         s, e = self.buckets[b]
-        op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
+        op = dist.ReduceOp.AVG if native_avg() else dist.ReduceOp.SUM
         self.works.append(dist.all_reduce(self.grad[s:e], op=op, async_op=True))
+        self.scaled.append(native_avg())
+
+    def wait_bucket(self, b):
+        """The current stream waits for bucket b's averaged gradients."""
+        self.works[b].wait()
+        if not self.scaled[b]:
+            s, e = self.buckets[b]
+            self.grad[s:e].mul_(1.0 / dist.get_world_size())
+            self.scaled[b] = True
 
     def ready(self, params):
         if not self.active:
@@ -142,10 +164,8 @@ class OverlappedAllReduce:
         if not self.active:
             return
         self.launch_remaining()
-        for w in self.works:
-            w.wait()
-        if dist.get_backend() != "nccl":
-            self.grad.mul_(1.0 / dist.get_world_size())
+        for b in range(len(self.works)):
+            self.wait_bucket(b)
         self.works = []
         self.active = False
 

@@ -13,6 +13,7 @@ Sources are (tensor, time_offset) pairs forming a virtual channel concat; the
 offset implements crop_and_concat (model.py:71-78).
 """
 import ctypes
+import os
 
 import torch
 
@@ -20,6 +21,8 @@ from . import _lib as L
 
 SLOPE = 0.01
 IN_EPS = 1e-5
+# dev-only A/B knob: force one K schedule on every GEMM (mst_conv_desc.splitk semantics)
+_FORCE_SPLITK = int(os.environ.get("MST_FORCE_SPLITK", "0"))
 
 
 def _lib():
@@ -114,7 +117,7 @@ def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt
     d.act = act
     d.drop_p = drop_p
     d.seed = seed
-    d.splitk = splitk
+    d.splitk = splitk or _FORCE_SPLITK
     ref = ctypes.byref(d)
     ws, nb = _workspace(lib.mst_conv_fwd_workspace_size(ref), A.device)
     _timed(lambda: L.check(lib.mst_conv_fwd_f32(ref, L.ptr(ws), nb, L.stream()), "mst_conv_fwd_f32"),
@@ -141,7 +144,7 @@ def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, ldc=0, ldt=0, scale=1
     d.ldc, d.ldt = ldc, ldt
     d.scale = scale
     d.accumulate = 1 if accumulate else 0
-    d.splitk = splitk
+    d.splitk = splitk or _FORCE_SPLITK
     ref = ctypes.byref(d)
     ws, nb = _workspace(lib.mst_wgrad_workspace_size(ref), P.device)
     _timed(lambda: L.check(lib.mst_conv_wgrad_f32(ref, L.ptr(ws), nb, L.stream()),
@@ -345,7 +348,3 @@ def scale_(x, s):
 
 def fill_(x, v):
     L.check(_lib().mst_fill_f32(L.ptr(x), x.numel(), v, L.stream()), "fill")
-
-
-def axpby_(x, y, a, b):
-    L.check(_lib().mst_axpby_f32(L.ptr(x), L.ptr(y), x.numel(), a, b, L.stream()), "axpby")

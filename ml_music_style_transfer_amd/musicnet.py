@@ -1,38 +1,42 @@
-"""MusicNet solo-piano filter (preprocessing/extract_piano_pieces_from_musicnet_dataset.py:10-24).
+"""Solo-piano selection over the MusicNet label files.
 
-A label file `<musicnet>/<data_type>_labels/<id>.csv` is a solo-piano piece when its
-`instrument` column holds exactly one distinct value, 1 (piano). The names of those CSV files
-are written one per line to `<output_file_basename>_<data_type>.txt`, in glob order like the
-reference. Host-side file filtering (pandas CSV reads), no device work.
+Drop-in for preprocessing/extract_piano_pieces_from_musicnet_dataset.py:10-24 (`main` keeps
+its three arguments and its output file). The rule: a piece is solo piano when every note row
+of its label CSV names instrument 1 and there is at least one row. The chosen CSV basenames go
+one per line, in glob order, to `<output_file_basename>_<data_type>.txt`. Host-side file work
+only (the csv module streams the one column; no device work, no pandas).
 """
+import csv
 import glob
 import os
 
-import pandas as pd
+PIANO = 1.0  # MusicNet's instrument code for acoustic piano
 
-PIANO_INSTRUMENT_LABEL = 1
+
+def instrument_codes(label_csv):
+    """The set of instrument codes in one MusicNet label file (its `instrument` column)."""
+    with open(label_csv, newline="") as fh:
+        return {float(row["instrument"]) for row in csv.DictReader(fh)}
+
+
+def is_solo_piano(label_csv):
+    return instrument_codes(label_csv) == {PIANO}
 
 
 def main(path_to_musicnet, data_type, output_file_basename):
-    path = os.path.join(path_to_musicnet, f"{data_type}_labels")
-    label_files = glob.glob(f"{path}/*.csv")
-    wav_file_list = []
-    for file in label_files:
-        instruments = list(set(pd.read_csv(file)['instrument'].values))
-        if len(instruments) == 1 and instruments[0] == PIANO_INSTRUMENT_LABEL:
-            wav_file_list.append(file)
-    out = output_file_basename + f"_{data_type}.txt"
-    with open(out, 'w') as f:
-        for item in wav_file_list:
-            f.write(f"{os.path.basename(item)}\n")
-    return [os.path.basename(p) for p in wav_file_list]
+    """Write and return the basenames of the solo-piano label files of one split."""
+    pattern = os.path.join(path_to_musicnet, data_type + "_labels", "*.csv")
+    chosen = [os.path.basename(f) for f in glob.glob(pattern) if is_solo_piano(f)]
+    with open(f"{output_file_basename}_{data_type}.txt", "w") as out:
+        out.writelines(name + "\n" for name in chosen)
+    return chosen
 
 
-if __name__ == '__main__':
+if __name__ == "__main__":
     import argparse
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--path-to-musicnet", default='../data/musicnet/')
-    ap.add_argument("--data-type", default='test', choices=['train', 'test'])
-    ap.add_argument("--output-file-basename", default='piano_pieces')
-    a = ap.parse_args()
+    cli = argparse.ArgumentParser(description="list the solo-piano pieces of a MusicNet split")
+    cli.add_argument("--path-to-musicnet", default="../data/musicnet/")
+    cli.add_argument("--data-type", default="test", choices=["train", "test"])
+    cli.add_argument("--output-file-basename", default="piano_pieces")
+    a = cli.parse_args()
     main(a.path_to_musicnet, a.data_type, a.output_file_basename)

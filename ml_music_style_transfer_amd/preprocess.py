@@ -226,16 +226,8 @@ def get_data(data_dir, dataset_outpath, data_type, debug=False, h=hp):
 
 
 def main(args):
-    """preprocess.py:203-215 (zip extraction, then get_data)."""
-    import os
-    import zipfile
-    if zipfile.is_zipfile(args.data_dir) is True:
-        print("Extracting zip file to local")
-        cwd = os.getcwd()
-        with zipfile.ZipFile(args.data_dir, 'r') as zip_ref:
-            root_data_dir = os.path.dirname(zip_ref.namelist()[0])
-            zip_ref.extractall(cwd)
-        args.data_dir = os.path.join(cwd, root_data_dir)
+    """preprocess.py:203-215 without its zip extraction (out of scope): `-data-dir`
+    is an already-extracted directory."""
     return get_data(args.data_dir, args.dataset_outpath, args.data_type, args.debug)
 
 

@@ -95,19 +95,39 @@ class Adam(torch.optim.Optimizer):
         return self
 
     def _flat_state(self, gi, pf, params):
+        """Flat m/v buffers (and the shared step count) of a flat-buffer group, built on first
+        use. Moments already in self.state (load_state_dict, or earlier per-parameter steps)
+        are copied into the flat slots. None when the parameters' step counts differ: the
+        per-parameter path then keeps torch's per-parameter bias correction."""
         key = (gi, pf.data_ptr())
         st = self._flat_groups.get(key)
         if st is None:
+            steps = {float(self.state[p]["step"]) for p in params
+                     if self.state.get(p, {}).get("exp_avg") is not None}
+            if len(steps) > 1 or (steps and any(
+                    self.state.get(p, {}).get("exp_avg") is None for p in params)):
+                return None
             m = torch.zeros_like(pf)
             v = torch.zeros_like(pf)
-            st = {"m": m, "v": v, "step": 0}
-            self._flat_groups[key] = st
+            st = {"m": m, "v": v, "step": int(steps.pop()) if steps else 0}
             index = self._owner._flat["index"]
             for p in params:
                 o, k = index[id(p)]
-                self.state[p] = {"step": None, "exp_avg": slot_view(m[o:o + k], p),
-                                 "exp_avg_sq": slot_view(v[o:o + k], p)}
+                mv, vv = slot_view(m[o:o + k], p), slot_view(v[o:o + k], p)
+                old = self.state.get(p, {})
+                if old.get("exp_avg") is not None:
+                    mv.copy_(old["exp_avg"])
+                    vv.copy_(old["exp_avg_sq"])
+                self.state[p] = {"step": torch.tensor(float(st["step"])), "exp_avg": mv,
+                                 "exp_avg_sq": vv}
+            self._flat_groups[key] = st
         return st
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict; the flat moment buffers are rebuilt from the
+        loaded per-parameter state on the next step (resume keeps exp_avg/exp_avg_sq/step)."""
+        super().load_state_dict(state_dict)
+        self._flat_groups = {}
 
     def _count_step(self, st, params):
         st["step"] += 1
@@ -136,9 +156,9 @@ class Adam(torch.optim.Optimizer):
             if not params:
                 continue
             flat = self._flat_of(group, params)
-            if flat is not None:
+            st = self._flat_state(gi, flat[0], params) if flat is not None else None
+            if st is not None:
                 pf, gf, n = flat
-                st = self._flat_state(gi, pf, params)
                 t = st["step"] + 1
                 bc1 = 1 - b1 ** t
                 bc2 = 1 - b2 ** t
@@ -149,16 +169,46 @@ class Adam(torch.optim.Optimizer):
                 state = self.state[p]
                 if len(state) == 0 or state.get("exp_avg") is None:
                     state["step"] = torch.tensor(0.0)
-                    state["exp_avg"] = torch.zeros_like(p)
+                    state["exp_avg"] = torch.zeros_like(p)  # p's strides (tap-major slots too)
                     state["exp_avg_sq"] = torch.zeros_like(p)
                 state["step"] += 1
                 t = float(state["step"])
                 bc1 = 1 - b1 ** t
                 bc2 = 1 - b2 ** t
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                K.adam(p.data, g, state["exp_avg"], state["exp_avg_sq"], lr / bc1, b1, b2, eps,
-                       math.sqrt(bc2))
+                _adam_param(p, state, lr / bc1, b1, b2, eps, math.sqrt(bc2))
         return loss
+
+
+def _memory_order(t):
+    """Dimension permutation that lists t's dims from the largest stride to the smallest: for a
+    dense tensor, t.permute(perm) is contiguous (a tap-major slot view (d0, d1, k) of (d0, k, d1)
+    memory gives perm (0, 2, 1))."""
+    return sorted(range(t.dim()), key=lambda d: (-t.stride(d), d))
+
+
+def _adam_param(p, state, lr_step, b1, b2, eps, bc2_sqrt):
+    """One parameter's update. adam_kernel walks raw memory, so p, its gradient and both
+    moments are handed over in p's memory order: the gradient (any layout) is permuted into it,
+    the moments are re-laid-out to p's strides once if they differ (e.g. loaded from a
+    checkpoint), and a non-dense p is updated through a contiguous copy."""
+    for key in ("exp_avg", "exp_avg_sq"):
+        x = state[key]
+        if x.stride() != p.stride():
+            y = torch.empty_like(p)
+            y.copy_(x)
+            state[key] = y
+    perm = _memory_order(p)
+    pv = p.data.permute(perm)
+    mv, vv = state["exp_avg"].permute(perm), state["exp_avg_sq"].permute(perm)
+    g = p.grad.permute(perm).contiguous()
+    if pv.is_contiguous() and mv.is_contiguous() and vv.is_contiguous():
+        K.adam(pv, g, mv, vv, lr_step, b1, b2, eps, bc2_sqrt)
+        return
+    pc, mc, vc = pv.contiguous(), mv.contiguous(), vv.contiguous()
+    K.adam(pc, g, mc, vc, lr_step, b1, b2, eps, bc2_sqrt)
+    pv.copy_(pc)
+    mv.copy_(mc)
+    vv.copy_(vc)
 
 
 class BackwardAdam:
@@ -176,7 +226,8 @@ class BackwardAdam:
 
     Inactive (step() runs the ordinary update) unless one parameter group holds exactly the
     model's flat parameters, and when gradients are reduced after backward (world > 1 without
-    an overlapped RCCL reducer, or a backend other than NCCL, which averages in finish())."""
+    an overlapped reducer). Any backend works: with gloo the reducer's per-bucket SUM is scaled
+    to the average on this side stream before the update (dp.OverlappedAllReduce.wait_bucket)."""
 
     def __init__(self, opt, model, bucket_bytes):
         self.opt = opt
@@ -207,8 +258,6 @@ class BackwardAdam:
             reducer = getattr(m, "_mst_dp", None)
             if reducer is None or reducer.buckets is not self.buckets:
                 return False
-            if torch.distributed.get_backend() != "nccl":
-                return False
         return True
 
     def begin(self):
@@ -220,6 +269,8 @@ class BackwardAdam:
         self.params = [p for p in group["params"] if id(p) in index]
         self.pf, self.gf, _ = self.model.flat_buffers()
         self.st = self.opt._flat_state(0, self.pf, self.params)
+        if self.st is None:
+            return
         b1, b2 = group["betas"]
         t = self.st["step"] + 1
         self.hp = (group["lr"] / (1 - b1 ** t), b1, b2, group["eps"], math.sqrt(1 - b2 ** t))
@@ -233,7 +284,7 @@ class BackwardAdam:
         compute = torch.cuda.current_stream()
         with torch.cuda.stream(self.stream):
             if reducer is not None and reducer.active:
-                reducer.works[b].wait()  # this stream waits for bucket b's all-reduce
+                reducer.wait_bucket(b)  # this stream waits for bucket b's averaged gradients
             else:
                 self.stream.wait_stream(compute)
             # one workgroup per CU: a background stream beside the backward GEMMs, which keep
@@ -381,7 +432,7 @@ def main(args, return_model=False):
     if world > 1:
         dp.broadcast_parameters(model)         # every rank starts from rank 0's weights
         dp.enable_overlapped_allreduce(model)  # bucket all-reduces inside backward
-        model._seed = rank << 24               # per-rank dropout streams
+        model._seed += rank << 24              # per-rank dropout streams
     optimizer = make_optimizer(model, lr=1e-3)
     model.zero_grad()
     optimizer.zero_grad()

@@ -8,8 +8,6 @@ CPU restatements of the reference's hot path (silburt/ML_Music_Style_Transfer):
                    tests/test_griffinlim.py:23, tests/plot_spec.py:20)
   midi_ref.py      framing constants, chunk formulas, piano-roll/onoff rules
                    (preprocessing/preprocess.py:17-42, 60-96, 118-160)
-  c/               plain-C restatements of the integer framing/onoff rules and a
-                   scalar DFT log-power (independent second oracle)
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
 anything here, and only as the checker / CPU baseline. The product package

@@ -10,7 +10,8 @@ Weights and inputs come from oracle.detinit (hash-based, framework
 independent), so fixtures store only outputs: losses, checksums, sampled
 entries and per-parameter gradient statistics.
 
-Usage:  python tests/golden/make_golden.py
+Usage:  python tests/golden/make_golden.py          (blocks, B=2/T=44, B=1/T=252)
+        python tests/golden/make_golden.py bench    (B=32/T=252, the benchmarked config)
 """
 import os
 import sys
@@ -133,6 +134,45 @@ def full_model(B, T, fname, adam=True):
     print("wrote", fname, "loss", loss.item(), "loss64", loss64.item())
 
 
+def full_model_lowmem(B, T, fname):
+    """full_model without Adam for a large batch (the benchmarked B=32, T=252): the fp32 and
+    fp64 reference runs happen one after the other so only one network is alive at a time."""
+    res = {}
+    for dtype in (torch.float32, torch.float64):
+        torch.manual_seed(0)
+        net = ref.PerformanceNet()
+        load_det(net)
+        net = net.to(dtype).eval()
+        y, loss, _ = _run(net, B, T, dtype)
+        res[dtype] = (y.detach().double().numpy().ravel(), loss.item(),
+                      {n: (p.grad.detach().double().numpy().ravel() if p.grad is not None else None)
+                       for n, p in net.named_parameters()})
+        del net, y
+    yv, loss, g32 = res[torch.float32]
+    yv64, loss64, g64s = res[torch.float64]
+    oidx = detinit.randint("outidx", (512,), 0, yv.size).astype(np.int64)
+    out = {"B": np.array(B), "T": np.array(T), "loss": np.array(loss, dtype=np.float64),
+           "loss64": np.array(loss64, dtype=np.float64),
+           "out_stat": np.array([yv.sum(), np.abs(yv).sum(), (yv * yv).sum()]),
+           "out_idx": oidx, "out_val": yv[oidx].astype(np.float32), "out_val64": yv64[oidx],
+           "out_shape": np.array([B, 1025, T])}
+    names = list(g32)
+    for n in names:
+        g, g64 = g32[n], g64s[n]
+        if g is None:
+            out[f"gnone:{n}"] = np.array(1)
+            continue
+        idx = sample_idx(n, g.size, 256)
+        out[f"gidx:{n}"] = idx
+        out[f"gval:{n}"] = g[idx].astype(np.float32)
+        out[f"gval64:{n}"] = g64[idx]
+        out[f"gstat:{n}"] = np.array([g.sum(), np.abs(g).sum(), (g * g).sum(),
+                                      np.linalg.norm(g - g64), np.linalg.norm(g64)])
+    out["param_names"] = np.array(names)
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print("wrote", fname, "loss", loss, "loss64", loss64)
+
+
 def blocks():
     """Small-shape per-block vectors (full tensors) for DownConv/UpConv/DenseConcat/MBR/crop."""
     out = {}
@@ -230,6 +270,9 @@ def blocks():
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["bench"]:  # the benchmarked configuration only (slow: ~minutes on CPU)
+        full_model_lowmem(32, 252, "full_B32_T252.npz")
+        sys.exit(0)
     blocks()
     full_model(2, 44, "full_B2_T44.npz")
     full_model(1, 252, "full_B1_T252.npz", adam=False)

@@ -156,3 +156,133 @@ def test_train_main_data_parallel_two_ranks(cuda, tmp_path, monkeypatch):
     torch.testing.assert_close(res[0][3], res[1][3], rtol=0, atol=0)
     exp = tmp_path / "experiments" / "piano_test"
     assert (exp / ("checkpoint-%d.tar" % res[0][2])).exists() and (exp / "hyperparams.json").exists()
+
+
+def _variants_worker(rank, world, port, q):
+    """Three data-parallel update paths on the same two steps, and gradient accumulation."""
+    import faulthandler
+    import sys
+    faulthandler.dump_traceback_later(280, exit=True, file=sys.stderr)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from ml_music_style_transfer_amd import _lib, dp
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd.model import PerformanceNet
+    from ml_music_style_transfer_amd.train import make_optimizer
+    from oracle import detinit
+    _lib.load()
+    dev = torch.device("cuda", 0)
+    xm, xa, cd, tg = [torch.from_numpy(a).to(dev) for a in detinit.model_inputs(1, 44)]
+    xa = xa * (1.0 + 0.5 * rank)           # different data per rank
+
+    def fresh():
+        torch.manual_seed(0)
+        net = PerformanceNet().to(dev).eval()   # eval: no dropout
+        dp.broadcast_parameters(net)
+        return net
+
+    def loss_of(net, k=0):
+        return E.l1_loss(net(xm, xa * (1.0 + 0.25 * k), cd), tg)
+
+    finals = {}
+    for mode in ("step", "backward_adam", "post"):
+        net = fresh()
+        if mode != "post":
+            dp.enable_overlapped_allreduce(net, bucket_bytes=64 << 20)
+        opt = make_optimizer(net, lr=1e-3, overlap_backward=(mode == "backward_adam"))
+        for _ in range(2):
+            opt.zero_grad()
+            loss_of(net).backward()
+            if mode == "post":
+                dp.allreduce_gradients(net)
+            opt.step()
+        if mode == "backward_adam":
+            assert opt._bwd.updates == 2  # the bucket updates ran inside backward, on gloo
+        finals[mode] = net.flat_buffers()[0].clone()
+        del net, opt
+    same = [torch.equal(finals["step"], finals[m]) for m in ("backward_adam", "post")]
+    n = finals["step"].numel()
+    idx = torch.randint(0, n, (NSAMP,), generator=torch.Generator().manual_seed(5)).to(dev)
+    sample = finals["step"][idx].cpu().numpy()  # numpy: pickled by value, no fd sharing
+    del finals
+
+    # gradient accumulation: two backward passes per step with the overlapped reducer equal the
+    # post-backward average of the accumulated local gradients
+    acc = {}
+    for mode in ("overlapped", "post"):
+        net = fresh()
+        if mode == "overlapped":
+            dp.enable_overlapped_allreduce(net, bucket_bytes=64 << 20)
+        net.zero_grad(set_to_none=True)
+        loss_of(net, 0).backward()
+        loss_of(net, 1).backward()
+        if mode == "post":
+            dp.allreduce_gradients(net)
+        else:
+            dp.finish_gradients(net)
+        acc[mode] = net.flat_buffers()[1][idx].cpu().numpy()
+        del net
+    torch.cuda.synchronize()
+    q.put((rank, same, sample, acc["overlapped"], acc["post"]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_update_paths_bitwise_two_ranks_one_gpu(cuda):
+    """Two ranks over gloo on one GPU exercise every data-parallel branch bench.py and train.main
+    take over RCCL: the overlapped bucket reducer with Adam in step(), BackwardAdam (each bucket's
+    update on a side stream right after that bucket's average, inside backward) and the
+    post-backward all-reduce. After two steps all three hold bitwise the same parameters, on
+    both ranks. With two backward passes before the exchange the overlapped reducer's result
+    equals the average of the accumulated gradients (fp32 rounding: 1e-5 relative)."""
+    import numpy as np
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_variants_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    deadline = time.monotonic() + 300
+    while len(res) < world:
+        try:
+            rank, *rest = q.get(timeout=5)
+            res[rank] = rest
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            if dead or time.monotonic() > deadline:
+                for p in procs:
+                    p.kill()
+                pytest.fail(f"worker failed (exit codes {dead})")
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for r in range(world):
+        same, sample, acc_o, acc_p = res[r]
+        assert same == [True, True], same
+        np.testing.assert_allclose(acc_o, acc_p, rtol=1e-5, atol=1e-9)
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+
+
+def test_bench_aux_two_ranks_one_gpu(tmp_path):
+    """bench_aux.py under torch.distributed.run with 2 ranks (gloo rehearsal on one GPU): every
+    rank takes its own clips, no data-path collective, one JSON line per workload from rank 0
+    with n_gpus 2 and value = both ranks' clips over the max-over-ranks time. Unmeasured on
+    xGMI hardware: this only proves the multi-rank harness runs."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MST_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench_aux.py"), "--workload", "frontend", "--clips", "16",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 2
+    for ln in lines:
+        assert ln["n_gpus"] == 2 and ln["value"] > 0 and ln["config"]["clips_per_gpu"] == 16
