@@ -168,16 +168,19 @@ int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, fl
                           void* stream);
 
 /* ---- Adam over a flat parameter buffer (torch.optim.Adam semantics, no weight decay) ----
- * At step t (1-based): lr_step = lr / (1 - b1^t); bc2_sqrt = sqrt(1 - b2^t) (NOT its inverse):
- *   m = m + (1-b1)(g - m);  v = b2 v + (1-b2) g^2;  p -= lr_step * m / (sqrt(v) / bc2_sqrt + eps).
+ * At step t (1-based): lr_step = lr / (1 - b1^t); bc2_sqrt = sqrt(1 - b2^t) (NOT its inverse);
+ * one_minus_b1 = 1 - b1 and one_minus_b2 = 1 - b2 computed in double by the caller and rounded,
+ * as torch does (1 - 0.999f in float would differ from torch's 0.001f by 1.3e-5 relative):
+ *   m = m + one_minus_b1 (g - m);  v = b2 v + one_minus_b2 g^2;
+ *   p -= lr_step * m / (sqrt(v) / bc2_sqrt + eps).
  * p, g, m, v: n floats each, 16-byte aligned, the same element order (any layout, shared). */
-int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
-                 float b2, float eps, float bc2_sqrt, void* stream);
+int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b2,
+                 float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt, void* stream);
 /* The same update over at most max_blocks 256-thread workgroups (grid-stride): a background
  * launch beside other kernels (one workgroup per CU leaves the GEMMs their occupancy). */
 int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
-                    float b1, float b2, float eps, float bc2_sqrt, int32_t max_blocks,
-                    void* stream);
+                    float b2, float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt,
+                    int32_t max_blocks, void* stream);
 
 /* ---- elementwise helpers ---- */
 int mst_scale_f32(float* x, int64_t n, float s, void* stream);

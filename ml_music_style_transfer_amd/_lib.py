@@ -74,9 +74,9 @@ SIGNATURES = {
     "mst_lrelu_bwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "mst_relu_gate_bwd_f32": (c_int32, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p]),
     "mst_adam_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
-                               c_float, c_float, c_float, c_void_p]),
+                               c_float, c_float, c_float, c_float, c_void_p]),
     "mst_adam_ex_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
-                                  c_float, c_float, c_float, c_float, c_int32, c_void_p]),
+                                  c_float, c_float, c_float, c_float, c_float, c_int32, c_void_p]),
     "mst_scale_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
     "mst_fill_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
     "mst_stft_logpow_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,

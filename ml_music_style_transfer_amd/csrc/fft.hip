@@ -7,8 +7,10 @@
 // holds 16 complex values and the 1024-point FFT runs as radix-16 (registers) ->
 // LDS transpose -> radix-16 (registers) -> LDS transpose -> radix-4, then the real-FFT
 // post-twist (X[k] from Z[k], Z[1024-k]) produces the 1025 bins. Row strides of the LDS
-// images are padded (68 complex) so every ds_read/ds_write_b64 lane group is
-// conflict-free. Twiddles come from a 512-entry quarter-wave LDS table
+// images are padded (68 complex); PMC showed this layout is NOT conflict-free (13.5 % of its
+// LDS cycles were bank conflicts, profiles/r01/pmc_stft_frontend.txt): the frequency-major
+// kernels below use fft1024_v2 instead (0 conflicts, profiles/r02). This round-1 path remains for
+// the frame-major complex STFT (Griffin-Lim) and the iSTFT. Twiddles come from a 512-entry quarter-wave LDS table
 // (W^(512q + r) = (-i)^q W^r), built in double precision on the host side of the
 // compiler (constexpr-free: computed once per workgroup with sincospi in f64).
 //
@@ -409,6 +411,503 @@ __global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// Frequency-major STFT (log-power / power / mel), the (B, F, T) layout of
+// process_spectrum_from_chunk (preprocess.py:47-49) and melspectrogram (plot_spec.py:20).
+//
+// Output. The round-1 kernel's (bin, 8 frames) 32-byte row pieces, written by one workgroup in
+// four rounds, cost ~90 of its 238 us for config 2 (profiles/r02/
+// stft_ablation_and_store_patterns.txt). The same bytes written as 64-byte pieces by
+// workgroups that all belong to ONE clip and share one XCD (its L2 merges the pieces of every
+// line before they reach HBM) run as fast as a contiguous write (38 us, 6.9 TB/s). So a
+// workgroup owns 16 consecutive frames of one clip, and workgroup g serves clip
+// (g / (8 nblk)) * 8 + g % 8 (g % 8 is the XCD group label), frames 16 ((g / 8) % nblk) + ...
+// Wave w computes frames w and 8 + w (the first one's results wait in registers); then the 16
+// frames go to LDS [frame][bin] and leave as (bin, 16 frames) rows, four float4 per bin.
+//
+// FFT (per wave, one frame): z[n] = x[2n] + i x[2n+1] windowed, n = l + 64 j (lane l, register
+// j), 1024 = 16 x 4 x 16:
+//   A  DFT16 over j in registers, twiddle W1024^(l k1) (LDS table);
+//   B1 DFT4 over the lane bits 4-5: two v_permlane{32,16}_swap stages exchange those lane bits
+//      with register bits 3-2 (no LDS), DFT4 in registers, twiddle W64^(l_lo q_lo);
+//   B2 one LDS transpose (XOR-swizzled, conflict-free both ways), DFT16 in registers: lane t
+//      ends with Z[t + 64 j] in register j.
+// The real-FFT post-twist pairs bin k = l + 64 j with 1024 - k, whose Z sits in lane 64 - l,
+// register 15 - j: 16 ds_bpermute (no LDS memory), one table twiddle per pair. One LDS round
+// trip per frame instead of three, twiddles from tables instead of product trees, and
+// log1p(p) = log(1 + p) on the hardware log (absolute error <= 1e-6, inside the 1e-4 bar).
+// ---------------------------------------------------------------------------
+constexpr int FPW = 16;            // frames per workgroup (max)
+#ifndef FM_WAVES
+#define FM_WAVES 8                 // frequency-major STFT: waves per workgroup (8 or 16)
+#endif
+constexpr int RSTR_MEL = 130;      // staging row stride for <= 128 mel bands (= 2 mod 32)
+
+// cos / sin of 2 pi m / n in double, evaluated at compile time (quadrant-reduced Taylor series)
+constexpr double kPiD = 3.14159265358979323846264338327950288;
+constexpr void cx_sincos_turn(long long m, long long n, double& c, double& s) {
+  m %= n;
+  if (m < 0) m += n;
+  const long long q = (4 * m) / n;                 // quadrant
+  const double x = (double)(4 * m - q * n) / (double)n * (kPiD / 2);  // [0, pi/2)
+  double x2 = x * x, ts = x, ss = x, tc = 1.0, sc = 1.0;
+  for (int k = 1; k < 16; ++k) {
+    ts *= -x2 / ((2.0 * k) * (2.0 * k + 1.0));
+    ss += ts;
+    tc *= -x2 / ((2.0 * k - 1.0) * (2.0 * k));
+    sc += tc;
+  }
+  const double cq[4] = {sc, -ss, -sc, ss}, sq[4] = {ss, sc, -ss, -sc};
+  c = cq[q];
+  s = sq[q];
+}
+struct FftTabs {
+  float2 a[15 * 64];  // a[(k1 - 1) 64 + l] = W1024^(l k1)
+  float2 b[3 * 16];   // b[(q - 1) 16 + l]  = W64^(l q)
+  float2 p[512];      // p[k] = W2048^k
+};
+constexpr FftTabs make_tabs() {
+  FftTabs t{};
+  double c = 0, s = 0;
+  for (int k1 = 1; k1 < 16; ++k1)
+    for (int l = 0; l < 64; ++l) {
+      cx_sincos_turn((long long)l * k1, 1024, c, s);
+      t.a[(k1 - 1) * 64 + l] = float2{(float)c, (float)-s};
+    }
+  for (int q = 1; q < 4; ++q)
+    for (int l = 0; l < 16; ++l) {
+      cx_sincos_turn((long long)l * q, 64, c, s);
+      t.b[(q - 1) * 16 + l] = float2{(float)c, (float)-s};
+    }
+  for (int k = 0; k < 512; ++k) {
+    cx_sincos_turn(k, 2048, c, s);
+    t.p[k] = float2{(float)c, (float)-s};
+  }
+  return t;
+}
+__device__ constexpr FftTabs kFftTabs = make_tabs();
+constexpr int TAB_F4 = (int)(sizeof(FftTabs) / 16);
+
+__device__ __forceinline__ void swap32(c2& lo, c2& hi) {  // lane bit 5 <-> the lo/hi pair
+  auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo.x), __float_as_uint(hi.x), false, false);
+  auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo.y), __float_as_uint(hi.y), false, false);
+  lo = mk(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
+  hi = mk(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+}
+__device__ __forceinline__ void swap16(c2& lo, c2& hi) {  // lane bit 4 <-> the lo/hi pair
+  auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo.x), __float_as_uint(hi.x), false, false);
+  auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(lo.y), __float_as_uint(hi.y), false, false);
+  lo = mk(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
+  hi = mk(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+}
+
+// Forward 1024-point FFT of one wave: v[j] = z[lane + 64 j] in, v[j] = Z[lane + 64 j] out.
+// S: this wave's 1024-entry LDS scratch; tabs: the LDS copy of kFftTabs.
+__device__ __forceinline__ void fft1024_v2(c2 v[16], c2* S, const FftTabs& tb, int lane) {
+  dft16<false>(v);  // Y[l][k1] in v[k1]
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) {
+    const float2 w = tb.a[(k1 - 1) * 64 + lane];
+    v[k1] = cmul(v[k1], mk(w.x, w.y));
+  }
+  // B1: lane bits (5, 4) <-> register bits (3, 2): lane (l_lo, k1 >> 2), register a + 4 l_hi
+#pragma unroll
+  for (int r = 0; r < 8; ++r) swap32(v[r], v[r + 8]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if ((r & 4) == 0) swap16(v[r], v[r + 4]);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) dft4<false>(v[a], v[a + 4], v[a + 8], v[a + 12]);  // -> q_lo
+  const int llo = lane & 15, c = lane >> 4;
+#pragma unroll
+  for (int q = 1; q < 4; ++q) {
+    const float2 w = tb.b[(q - 1) * 16 + llo];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) v[a + 4 * q] = cmul(v[a + 4 * q], mk(w.x, w.y));
+  }
+  // B2: pair p = k1 + 16 q_lo (k1 = a + 4 c) gathers its 16 l_lo values in lane p. Pairs are
+  // 17 entries apart: the writes (16 lanes per pair) and the reads (lane t, entry i) are
+  // bank-conflict-free, and every address is a per-lane base plus an immediate offset.
+  c2* Sw = S + 68 * c + llo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Sw[17 * (a + 16 * q)] = v[a + 4 * q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const c2* Sr = S + 17 * lane;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = Sr[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  dft16<false>(v);  // Z[lane + 64 q_hi] in v[q_hi]
+}
+
+__device__ __forceinline__ float bperm(int src_byte, float x) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_byte, __float_as_int(x)));
+}
+
+__device__ __forceinline__ float ln_1p_quarter(float p4) {  // log1p(p4 / 4)
+  return __log2f(fmaf(0.25f, p4, 1.f)) * 0.69314718055994531f;
+}
+
+// Power spectrum from Z[lane + 64 j] in v, as bin pairs: r[2j] = bin l + 64 j, r[2j + 1] =
+// bin 1024 - l - 64 j (j = 0..7), r[16] = bin 512 (meaningful in lane 0); LOG: log1p(power).
+// 2 X[k] = E + W^k D, 2 conj(X[1024 - k]) = E - W^k D with E = Z[k] + conj(Z[1024 - k]),
+// D = -i (Z[k] - conj(Z[1024 - k])); Z[1024 - k] lives in lane 64 - l, register 15 - j.
+template <bool LOG>
+__device__ __forceinline__ void power_pairs_v2(const c2 v[16], const FftTabs& tb, int lane,
+                                               float r[17]) {
+  const int src = ((64 - lane) & 63) * 4;
+  c2 prev = v[0];  // lane 0's partner 1024 - 64 j is its own v[16 - j] (v[0] for j = 0)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const c2 bpj = mk(bperm(src, v[15 - j].x), bperm(src, v[15 - j].y));
+    const c2 Bq = lane == 0 ? prev : bpj;
+    prev = bpj;
+    const c2 A = v[j];
+    const c2 E = mk(A.x + Bq.x, A.y - Bq.y);
+    const c2 D = mk(A.y + Bq.y, Bq.x - A.x);  // -i (A - conj(Bq))
+    const float2 w = tb.p[lane + 64 * j];
+    const c2 TD = cmul(mk(w.x, w.y), D);
+    const c2 P = E + TD, M = E - TD;
+    const float p4 = P.x * P.x + P.y * P.y, m4 = M.x * M.x + M.y * M.y;
+    r[2 * j] = LOG ? ln_1p_quarter(p4) : 0.25f * p4;
+    r[2 * j + 1] = LOG ? ln_1p_quarter(m4) : 0.25f * m4;
+  }
+  const float z4 = 4.f * (v[8].x * v[8].x + v[8].y * v[8].y);
+  r[16] = LOG ? ln_1p_quarter(z4) : 0.25f * z4;
+}
+
+// staging position of (frame row, bin k < 1024): row stride 1024, bits of k XORed with the row's
+// quad index so the write-out's 4-row column gathers are bank-conflict-free (16 rows: 8 bins x
+// 4 quads per 32 lanes, XOR 8 q; 8 rows: 16 bins x 2 quads, XOR 16 q)
+template <int ROWS>
+__device__ __forceinline__ int stage_pos(int row, int k) {
+  return row * 1024 + (k ^ ((ROWS == 16 ? 8 : 16) * ((row >> 2) & (ROWS / 4 - 1))));
+}
+
+// Raw samples of frame f as z[lane + 64 j] = (x_pad[s0 + 2n], x_pad[s0 + 2n + 1]), n = lane + 64 j,
+// s0 = f hop - 1024, center padding reflect or zeros. Exactly 16 buffer loads on every path and
+// no use of the loaded data here (the callers' vmcnt accounting depends on both): a frame that
+// touches the padding loads per-lane pairs and records what fix_frame must do with them. A
+// reflected pair is an adjacent pair read backwards: x_pad[s] = x[-s] (s < 0) and
+// x[2 L - 2 - s] (s >= L), so (x_pad[s], x_pad[s + 1]) is the pair at -s - 1 or at
+// 2 L - 3 - s, swapped; zero padding loads the clamped pair and drops the outside halves.
+struct FrameFix {
+  unsigned swap;  // bit j: swap pair j (reflect)
+  unsigned zlo;   // bit j: pair j's first sample is padding (zeros)
+  unsigned zhi;   // bit j: its second sample is padding
+  unsigned sel;   // bit j: the wanted first sample is the loaded pair's second (zeros, clamped)
+  int edge;       // wave-uniform: the frame touches the padding
+};
+
+__device__ __forceinline__ void fetch_frame16(const float* xr, int L, int f, int hop, int pad_mode,
+                                              int lane, float2 raw[16], FrameFix& fx) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xr), (short)0, L * 4, 0x00020000);
+  const int s0 = f * hop - NFFT / 2;
+  fx.edge = !(s0 >= 0 && s0 + NFFT <= L);
+  fx.swap = fx.zlo = fx.zhi = fx.sel = 0;
+  if (!fx.edge) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      raw[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, 8 * lane, 4 * s0 + 512 * j, 0));
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int s = s0 + 2 * (lane + 64 * j);
+      int a;
+      if (pad_mode == MST_PAD_REFLECT) {
+        const bool left = s < 0, right = s + 1 >= L;
+        a = left ? -s - 1 : (right ? 2 * L - 3 - s : s);
+        fx.swap |= (unsigned)(left || right) << j;
+      } else {
+        a = min(max(s, 0), L - 2);
+        fx.zlo |= (unsigned)(s < 0 || s >= L) << j;
+        fx.zhi |= (unsigned)(s + 1 < 0 || s + 1 >= L) << j;
+        fx.sel |= (unsigned)(s == a + 1) << j;  // only at the right end: (x[L-1], 0)
+      }
+      raw[j] = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, 4 * a, 0, 0));
+    }
+  }
+}
+
+__device__ __forceinline__ void fix_frame(float2 raw[16], const FrameFix& fx) {
+  if (!fx.edge) return;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const float2 p = raw[j];
+    float lo = ((fx.swap | fx.sel) >> j) & 1 ? p.y : p.x;
+    float hi = (fx.swap >> j) & 1 ? p.x : p.y;
+    if ((fx.zlo >> j) & 1) lo = 0.f;
+    if ((fx.zhi >> j) & 1) hi = 0.f;
+    raw[j] = make_float2(lo, hi);
+  }
+}
+
+// Persistent workgroups, one per CU: 16 waves, one frame each per 16-frame block. WG g serves
+// XCD group x = g % 8, i.e. clips x, x + 8, ..., walking that group's (clip, block) list with
+// stride W (WGs per group): at any moment a group's WGs work on a few whole clips, whose row
+// pieces the group's L2 merges.
+//
+// Input: a block's 16 frames span (15 hop + 2048) samples (23.5 KB at hop 256) but fetching
+// every frame separately moves 128 KB through the load path, 8x over; the round-2 stamps
+// (tools/micro/stft_stamps.hip) had the per-wave prefetch issue alone at ~4.9k cycles per
+// block. So the next block's span is DMA'd into LDS (buffer_load ... lds, 1 KB per
+// instruction, out-of-range reads give the zero padding, per-sample sources the reflect
+// padding) during the staging phase, into the scratch half the staging does not use, and each
+// wave reads its frame from there at the start of the block.
+//
+// Stores and loads (LDS-DMA included) share vmcnt and complete in issue order, so the DMA is
+// issued before the write-out, the write-out is a fixed count NST of buffer stores (dropped
+// out-of-range offsets instead of branches), the loop entry issues NST dropped stores too, and
+// the top of the loop waits vmcnt(NST): its own DMA has landed, the previous block's stores
+// stay in flight. Barriers are raw s_barrier + lgkmcnt(0): __syncthreads() would drain vmcnt.
+// FMW (template): waves per workgroup = frames per block, 16 (one workgroup per CU) or 8 (two)
+#ifdef STFT_STAMPS  // dev instrumentation (tools/micro/stft_stamps.hip)
+__device__ unsigned long long g_stamps[512 * 16 * 16 * 16];
+#define STAMP(i) do { if (lane == 0 && blockIdx.x < 512 && it < 16) \
+    g_stamps[((blockIdx.x * 16 + (threadIdx.x >> 6)) * 16 + it) * 16 + (i)] = clock64(); } while (0)
+#else
+#define STAMP(i) do { } while (0)
+#endif
+#define LDS_BARRIER() do { __builtin_amdgcn_s_waitcnt(0xc07f); __builtin_amdgcn_s_barrier(); } while (0)
+
+// LDS-DMA in inline asm (cdna_hip_programming.md 5.7): hipcc does not model the asm, so it neither
+// counts it nor drains it before later LDS accesses (as a builtin DMA it would insert vmcnt(0)
+// before every LDS access that may alias, waiting for the write-out's stores as well); the
+// kernel waits for it itself (vmcnt(NST), then a barrier, then the reads). M0 is written and
+// restored inside the statement.
+__device__ __forceinline__ void dma_b128(__amdgpu_buffer_rsrc_t rs, unsigned lds_addr, int voff, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
+__device__ __forceinline__ void dma_b32(__amdgpu_buffer_rsrc_t rs, unsigned lds_addr, int voff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr)
+      : "memory");
+}
+
+// DMA the span of a block (samples s_lo .. s_lo + sp of clip xr, padded) into LDS span[], spread
+// over the workgroup's waves. Interior blocks with a 16-byte aligned start move 16 B per lane;
+// the others one sample per lane from its own source (reflect), or from out of range (zeros).
+template <int FMW>
+__device__ __forceinline__ void load_span(const float* xr, int L, int s_lo, int sp, int pad_mode,
+                                          float* span, int wave, int lane) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xr), (short)0, L * 4, 0x00020000);
+  const unsigned base = (unsigned)(uintptr_t)span;  // LDS byte address (low half of the flat one)
+  const bool fast = s_lo >= 0 && s_lo + sp <= L && ((((uintptr_t)(xr + s_lo)) & 15) == 0);
+  if (fast) {
+    for (int i = wave; i * 256 < sp; i += FMW)
+      dma_b128(rs, __builtin_amdgcn_readfirstlane(base + 1024 * i), 16 * lane,
+               __builtin_amdgcn_readfirstlane(4 * s_lo + 1024 * i));
+  } else {
+    for (int i = wave; i * 64 < sp; i += FMW) {
+      const int s = s_lo + 64 * i + lane;
+      int src;
+      if (pad_mode == MST_PAD_REFLECT) src = s < 0 ? -s : (s >= L ? 2 * (L - 1) - s : s);
+      else src = (s < 0 || s >= L) ? L : s;  // L: out of range, reads 0
+      dma_b32(rs, __builtin_amdgcn_readfirstlane(base + 256 * i), 4 * src);
+    }
+  }
+}
+
+template <int MODE, bool V4, int FMW>
+__global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __restrict__ x, int B,
+                                                               int L, int T, int hop, int pad_mode,
+                                                               float* __restrict__ out, MelTab mel,
+                                                               int W) {
+  // FMW x 8,704 B scratch + 12,160 B of tables: 151,424 B (16 waves, one workgroup per CU) or
+  // 81,792 B (8 waves, two per CU)
+  __shared__ __attribute__((aligned(16))) c2 scratch[FMW * SCR];
+  __shared__ __attribute__((aligned(16))) FftTabs tb;
+  constexpr int FPB = FMW;                // frames per block
+  constexpr int SPAN_OFF = FPB * NC * 4;  // bytes: the span sits after the staging rows
+  const int nblk = (T + FPB - 1) / FPB;
+  const int xg = blockIdx.x & 7, wi = blockIdx.x >> 3;
+  const int U = (B - xg + 7) / 8 * nblk;  // blocks of this XCD group
+  if (wi >= U) return;                    // whole workgroup: before any barrier
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  {
+    const float4* src = reinterpret_cast<const float4*>(&kFftTabs);
+    float4* dst = reinterpret_cast<float4*>(&tb);
+    for (int i = threadIdx.x; i < TAB_F4; i += blockDim.x) dst[i] = src[i];
+  }
+  c2* S = scratch + wave * SCR;
+  float* Sf = reinterpret_cast<float*>(scratch);
+  float* span = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + SPAN_OFF);
+  const int sp = (FPB - 1) * hop + NFFT;  // span samples (launcher: fits after the staging)
+  constexpr bool MELM = MODE == MODE_MEL;
+  const int nrows = MELM ? mel.n_mels : NB;
+  const int clip_bytes = nrows * T * 4;  // < 2^31: checked by the launcher
+  // this lane's 32 window weights (Hann at samples 2n, 2n + 1, n = lane + 64 j), kept in
+  // registers for the whole kernel (80 -> 112 VGPRs, still 4 waves per SIMD): 32 multiplies
+  // per frame instead of ~110 instructions recomputing them
+  float wwe[16], wwo[16];
+  {
+    const int lane = threadIdx.x & 63;
+    double sn, cs;
+    sincospi((2.0 * lane) / 2048.0, &sn, &cs);
+    const c2 e1 = mk((float)cs, (float)-sn);
+    sincospi((2.0 * lane + 1.0) / 2048.0, &sn, &cs);
+    const c2 eh = mk((float)cs, (float)-sn);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      wwe[j] = hann_sq(e1, j);
+      wwo[j] = hann_sq(eh, j);
+    }
+  }
+  const long long rowT = T;
+  auto clip_of = [&](int u) { return xg + 8 * (u / nblk); };
+  auto frame0_of = [&](int u) { return (u % nblk) * FPB; };
+  constexpr int NST = MELM ? 1 : 5;  // write-out stores per thread per block (V4)
+  constexpr int VM_NST = 0x0f70 | (NST & 15);  // s_waitcnt vmcnt(NST), expcnt/lgkmcnt unmasked
+
+  load_span<FMW>(x + (long long)clip_of(wi) * L, L, frame0_of(wi) * hop - NFFT / 2, sp, pad_mode, span,
+            wave, threadIdx.x & 63);
+  if (V4) {  // the loop body's store tail, dropped (zero-size descriptor); distinct offsets so
+            // none of them is merged away: the loop-top vmcnt(NST) counts exactly NST stores
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NST; ++i) __builtin_amdgcn_raw_buffer_store_b32(0, rs, 16 * i, 0, 0);
+  }
+#pragma unroll 1
+  for (int u = wi, it = 0; u < U; u += W, ++it) {
+    // every lane-derived value below is recomputed per block from a laundered thread index and
+    // laundered window phases / table offset: hoisted out of the loop they outnumber the free
+    // registers and the kernel spills
+    int tid = threadIdx.x, toff = 0;
+    __asm__ volatile("" : "+v"(tid), "+v"(toff));
+    const FftTabs& tbl = *reinterpret_cast<const FftTabs*>(reinterpret_cast<const char*>(&tb) + toff);
+    const int lane = tid & 63;
+    STAMP(0);
+    if (V4) __builtin_amdgcn_s_waitcnt(VM_NST);  // this wave's span DMA has landed
+    else __builtin_amdgcn_s_waitcnt(0x0f70);
+    LDS_BARRIER();  // every wave's DMA landed; the previous block's staging is read out
+    const int b = clip_of(u), f0 = frame0_of(u);
+    const int nfr = min(FPB, T - f0);
+    const int fl = wave;
+    float2 raw[16];
+    {
+      const float2* src = reinterpret_cast<const float2*>(span + fl * hop) + lane;  // hop even
+#pragma unroll
+      for (int j = 0; j < 16; ++j) raw[j] = src[64 * j];
+    }
+    LDS_BARRIER();  // the span is read: the FFT scratch may overwrite it
+    STAMP(1);
+    float res[17];
+    if (fl < nfr) {
+      c2 v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = mk(raw[j].x * wwe[j], raw[j].y * wwo[j]);
+      fft1024_v2(v, S, tbl, lane);
+      if (!MELM) {
+        power_pairs_v2<MODE == MODE_LOGPOW>(v, tbl, lane, res);
+      } else {
+        float r[17];
+        power_pairs_v2<false>(v, tbl, lane, r);
+        // power spectrum into this wave's scratch (its FFT reads are done), then two mel bands
+        // per lane
+        float* P = reinterpret_cast<float*>(S);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          P[lane + 64 * j] = r[2 * j];
+          P[NC - lane - 64 * j] = r[2 * j + 1];
+        }
+        if (lane == 0) P[NC / 2] = r[16];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int m = lane + 64 * q;
+          float acc = 0.f;
+          if (m < mel.n_mels) {
+            const int st = mel.start[m], n = mel.len[m], wo2 = mel.woff[m];
+            for (int i = 0; i < n; ++i) acc += mel.w[wo2 + i] * P[st + i];
+          }
+          res[q] = acc;
+        }
+      }
+    }
+    STAMP(2);
+    LDS_BARRIER();  // every FFT is done: the scratch becomes staging + the next span
+    STAMP(3);
+    {
+      const int un = u + W;
+      if (un < U)
+        load_span<FMW>(x + (long long)clip_of(un) * L, L, frame0_of(un) * hop - NFFT / 2, sp, pad_mode,
+                  span, wave, lane);
+    }
+    STAMP(7);
+    if (fl < nfr) {
+      if (!MELM) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          Sf[stage_pos<FPB>(fl, lane + 64 * j)] = res[2 * j];
+          if (lane + j > 0) Sf[stage_pos<FPB>(fl, NC - lane - 64 * j)] = res[2 * j + 1];
+        }
+        if (lane == 0) Sf[stage_pos<FPB>(fl, NC / 2)] = res[16];
+      } else {
+        float* row = Sf + fl * RSTR_MEL;
+        row[lane] = res[0];
+        row[lane + 64] = res[1];
+      }
+    }
+    STAMP(8);
+    LDS_BARRIER();
+    STAMP(4);
+    const int nr = MELM ? mel.n_mels : NC;  // staged rows (bin 1024 goes straight out)
+    float* oc = out + (long long)b * nrows * rowT;
+    if (V4) {
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(oc, (short)0, clip_bytes, 0x00020000);
+      constexpr int NQ = FPB / 4;  // 4-frame quads per row
+      const int q = tid & (NQ - 1);
+      // (row, quad) items: 1024 x NQ over 64 FMW threads = four per thread (MELM: 128 x NQ, one
+      // for FMW = 16 and NQ * 128 / 512 = one for FMW = 8)
+#pragma unroll
+      for (int i = 0; i < (MELM ? 1 : 4); ++i) {
+        const int k = tid / NQ + (64 * FMW / NQ) * i;
+        float vv[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+          vv[w] = MELM ? Sf[(4 * q + w) * RSTR_MEL + k] : Sf[stage_pos<FPB>(4 * q + w, k)];
+        const bool ok = k < nr && 4 * q + 3 < nfr;
+        const int off = ok ? (int)((k * rowT + f0 + 4 * q) * 4) : clip_bytes;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                               make_float4(vv[0], vv[1], vv[2], vv[3])),
+            rs, off, 0, 0);
+      }
+      if (!MELM) {  // bin 1024 of this wave's frame (lane 0 holds it)
+        const int off = (lane == 0 && fl < nfr) ? (int)((NC * rowT + f0 + fl) * 4) : clip_bytes;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(res[1]), rs, off, 0, 0);
+      }
+    } else {
+      float* ob = oc + f0;
+      for (int e = tid; e < nr * (FPB / 4); e += blockDim.x) {
+        const int k = e / (FPB / 4), q = e % (FPB / 4);
+        for (int w = 0; w < 4 && 4 * q + w < nfr; ++w)
+          ob[(long long)k * rowT + 4 * q + w] =
+              MELM ? Sf[(4 * q + w) * RSTR_MEL + k] : Sf[stage_pos<FPB>(4 * q + w, k)];
+      }
+      if (!MELM && lane == 0 && fl < nfr) ob[NC * rowT + fl] = res[1];
+    }
+    STAMP(5);
+    STAMP(6);
+  }
+}
+#undef STAMP
+#undef LDS_BARRIER
+
+// ---------------------------------------------------------------------------
 // iSTFT (librosa.istft, center=True, Hann): workgroup = 512 threads, output segment of
 // SEG = 16 samples per thread. Frames overlapping the segment are inverse-FFT'd 8 at a
 // time (one per wave) into the waves' scratch; every thread then accumulates its own
@@ -775,12 +1274,33 @@ int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int 
   MST_REQUIRE(L > NFFT / 2 || pad_mode == MST_PAD_CONSTANT);
   MST_REQUIRE(pad_mode == MST_PAD_REFLECT || pad_mode == MST_PAD_CONSTANT);
   const int T = 1 + L / hop;
-  dim3 grid(ceil_div(T, FR), B), block(512);
-  switch (mode) {
-    case MODE_LOGPOW: hipLaunchKernelGGL(stft_kernel<MODE_LOGPOW>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
-    case MODE_POWER: hipLaunchKernelGGL(stft_kernel<MODE_POWER>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
-    case MODE_MEL: hipLaunchKernelGGL(stft_kernel<MODE_MEL>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
-    default: hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+  if (mode == MODE_COMPLEX) {  // frame-major (B, T, F, 2): each frame's spectrum is contiguous
+    dim3 grid(ceil_div(T, FR), B), block(512);
+    hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel);
+  } else if ((hop & 1) || (long long)((FM_WAVES - 1) * hop + NFFT) * 4 > (long long)FM_WAVES * (SCR * 8 - NC * 4)) {
+    // odd hops (8-byte span reads) or spans beyond the scratch: the round-1 kernel
+    dim3 grid(ceil_div(T, FR), B), block(512);
+    switch (mode) {
+      case MODE_LOGPOW: hipLaunchKernelGGL(stft_kernel<MODE_LOGPOW>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+      case MODE_POWER: hipLaunchKernelGGL(stft_kernel<MODE_POWER>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+      default: hipLaunchKernelGGL(stft_kernel<MODE_MEL>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel); break;
+    }
+  } else {  // frequency-major: persistent XCD-grouped workgroups over FM_WAVES-frame blocks
+    // resident workgroups: 256 CUs x (1024 threads: one, 512: two), i.e. 32 or 64 per XCD group
+    const long long per_group = (long long)ceil_div(B, 8) * ceil_div(T, FM_WAVES);
+    const int wmax = FM_WAVES == 16 ? 32 : 64;
+    const int W = (int)(per_group < wmax ? per_group : wmax);
+    dim3 grid(8 * W), block(64 * FM_WAVES);
+    const long long rows = mode == MODE_MEL ? mel.n_mels : NB;
+    MST_REQUIRE(rows * T * 4 < (1ll << 31));  // per-clip buffer descriptors
+    const bool v4 = (T & 3) == 0 && ((uintptr_t)out & 15) == 0;
+#define MST_STFT_FM(M, V) hipLaunchKernelGGL((stft_fm_kernel<M, V, FM_WAVES>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W)
+    switch (mode) {
+      case MODE_LOGPOW: if (v4) MST_STFT_FM(MODE_LOGPOW, true); else MST_STFT_FM(MODE_LOGPOW, false); break;
+      case MODE_POWER: if (v4) MST_STFT_FM(MODE_POWER, true); else MST_STFT_FM(MODE_POWER, false); break;
+      default: if (v4) MST_STFT_FM(MODE_MEL, true); else MST_STFT_FM(MODE_MEL, false); break;
+    }
+#undef MST_STFT_FM
   }
   MST_CHECK_LAUNCH();
   return MST_OK;

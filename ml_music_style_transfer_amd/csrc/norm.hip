@@ -297,9 +297,8 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const double* __restric
 // p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps). Vectorised 4-wide over the flat buffer.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
-                                                   long long n, float lr_step, float b1, float b2,
-                                                   float eps, float bc2_sqrt) {
-  const float w1 = 1.f - b1, w2 = 1.f - b2;
+                                                   long long n, float lr_step, float b2, float w1,
+                                                   float w2, float eps, float bc2_sqrt) {
   long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -499,19 +498,21 @@ int mst_relu_gate_bwd_f32(const float* d, const float* h, int64_t n, float s, fl
 }
 
 int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
-                    float b1, float b2, float eps, float bc2_sqrt, int32_t max_blocks,
-                    void* stream) {
+                    float b2, float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt,
+                    int32_t max_blocks, void* stream) {
   MST_REQUIRE(p && g && m && v && n > 0 && max_blocks > 0);
   MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, max_blocks)), dim3(256), 0,
-                     (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b1, b2, eps, bc2_sqrt);
+                     (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b2, one_minus_b1,
+                     one_minus_b2, eps, bc2_sqrt);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
 
-int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b1,
-                 float b2, float eps, float bc2_sqrt, void* stream) {
-  return mst_adam_ex_f32(p, g, m, v, n, lr_step, b1, b2, eps, bc2_sqrt, 16384, stream);
+int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b2,
+                 float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt, void* stream) {
+  return mst_adam_ex_f32(p, g, m, v, n, lr_step, b2, one_minus_b1, one_minus_b2, eps, bc2_sqrt,
+                         16384, stream);
 }
 
 int mst_scale_f32(float* x, int64_t n, float s, void* stream) {

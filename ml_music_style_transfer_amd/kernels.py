@@ -333,13 +333,14 @@ def l1_bwd(pred, target, gscale):
 
 
 def adam(p, g, m, v, lr_step, b1, b2, eps, bc2_sqrt, max_blocks=None):
-    """max_blocks caps the grid (a background launch beside other kernels)."""
+    """torch.optim.Adam's update (mst_adam_f32). 1 - b1 and 1 - b2 are formed in double here and
+    rounded, as torch forms them; max_blocks caps the grid (a background launch)."""
+    args = (L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step, b2, 1.0 - b1, 1.0 - b2, eps,
+            bc2_sqrt)
     if max_blocks is None:
-        L.check(_lib().mst_adam_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step, b1,
-                                    b2, eps, bc2_sqrt, L.stream()), "adam")
+        L.check(_lib().mst_adam_f32(*args, L.stream()), "adam")
     else:
-        L.check(_lib().mst_adam_ex_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), lr_step,
-                                       b1, b2, eps, bc2_sqrt, max_blocks, L.stream()), "adam")
+        L.check(_lib().mst_adam_ex_f32(*args, max_blocks, L.stream()), "adam")
 
 
 def scale_(x, s):
