@@ -90,10 +90,29 @@ def _event_ms(fn, reps=5):
     return s.elapsed_time(e) / reps
 
 
-def _roof(achieved_gbs, kernel, bytes_per_launch):
-    return {"bound": "hbm", "kernel": kernel, "achieved": round(achieved_gbs, 1),
-            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-            "traffic": None, "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+def _measured_traffic(kernel_key):
+    """HBM bytes per launch of a kernel from the newest round's PMC passes (tools/pmc_traffic.py:
+    2 x FETCH_SIZE + WRITE_SIZE over `rocprofv3 --pmc` runs of this script), or (None, None)."""
+    pdir = os.path.join(ROOT, "profiles")
+    for r in sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) if os.path.isdir(pdir) else []:
+        tj = os.path.join(pdir, r, "stft_traffic.json")
+        if os.path.exists(tj):
+            d = json.load(open(tj))
+            for k, v in d.get("per_kernel", {}).items():
+                if kernel_key in k:
+                    return round(2 * v["fetch_raw_per_launch"] + v["write_per_launch"]), \
+                        f"profiles/{r}/stft_traffic.json ({d.get('build', '')})"
+    return None, None
+
+
+def _roof(achieved_gbs, kernel, bytes_per_launch, traffic_key=None):
+    traffic, src = _measured_traffic(traffic_key) if traffic_key else (None, None)
+    out = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved_gbs, 1),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+           "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch)}
+    if src:
+        out["traffic_source"] = src
+    return out
 
 
 def _line(metric, value, unit, world, steps, warmup, ms, config, roofline, cpu, extra=None):
@@ -149,11 +168,11 @@ def frontend(args, world, rank, dev):
     x, _ = bench.synth_clips(B, 4242 + 100_000 * rank)
     xd = torch.from_numpy(x).to(dev)
     res = []
-    for name, fn, bpc, kern in (
+    for name, fn, bpc, kern, tkey in (
             ("logpow", lambda: spectral.stft_logpow(xd, hop=bench.HOP), 4 * L + 4 * F * T,
-             "stft_kernel<LOGPOW>"),
+             "stft_fm_kernel<LOGPOW> (fft.hip)", "stft_fm_kernel<0,"),
             ("mel", lambda: spectral.melspectrogram(xd, bench.SR, hop_length=bench.HOP), 4 * L + 4 * M * T,
-             "stft_kernel<MEL>")):
+             "stft_fm_kernel<MEL> (fft.hip)", "stft_fm_kernel<2,")):
         dt = _timed(fn, args.steps, args.warmup, world)
         kms = _event_ms(fn)
         cpu = None
@@ -175,7 +194,8 @@ def frontend(args, world, rank, dev):
                          args.steps, args.warmup, dt * 1e3,
                          {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,
                           "n_fft": 2048, "hop": bench.HOP},
-                         _roof(B * bpc / (kms * 1e-3) / 1e9, kern, B * bpc), cpu,
+                         _roof(B * bpc / (kms * 1e-3) / 1e9, kern, B * bpc,
+                               tkey if B == 256 else None), cpu,
                          {"kernel_ms": round(kms, 4)}))
     return res
 

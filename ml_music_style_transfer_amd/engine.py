@@ -43,11 +43,20 @@ class GradSink:
 
     `on_ready(params)` (optional) is told, at each block boundary of the backward program,
     which parameters' gradient kernels have all been launched on the current stream; the
-    data-parallel reducer (dp.OverlappedAllReduce) starts bucket all-reduces from it."""
+    data-parallel reducer (dp.OverlappedAllReduce) starts bucket all-reduces from it.
 
-    def __init__(self, flat_grad_of=None, on_ready=None):
+    Weight-gradient GEMMs are off the backward's critical path (the next layer needs only the
+    input gradient), so with a side stream (`side`) they run there, concurrently with the
+    input-gradient GEMMs and norm kernels of the main stream: a GEMM's trailing partial wave of
+    workgroups no longer leaves the chip half idle. Tensors a side launch reads are recorded on
+    the side stream (the caching allocator must not hand them out again before it is done), and
+    the main stream waits for the side stream before the block listeners run and at the end."""
+
+    def __init__(self, flat_grad_of=None, on_ready=None, side=None):
         self.flat_grad_of = flat_grad_of or (lambda p: None)
         self.on_ready = on_ready
+        self.side = side
+        self._side_pending = False
         self._pending = []
 
     def target(self, p):
@@ -60,8 +69,27 @@ class GradSink:
             return g, False
         return p.grad, True
 
+    def wgrad(self, launch, *reads):
+        """Run a weight-gradient launch (on the side stream when there is one)."""
+        if self.side is None:
+            launch()
+            return
+        main = torch.cuda.current_stream()
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            launch()
+        for t in reads:
+            t.record_stream(self.side)
+        self._side_pending = True
+
+    def join(self):
+        if self._side_pending:
+            torch.cuda.current_stream().wait_stream(self.side)
+            self._side_pending = False
+
     def block_done(self):
         if self.on_ready is not None and self._pending:
+            self.join()
             self.on_ready(self._pending)
         self._pending = []
 
@@ -86,7 +114,7 @@ def downconv_bwd(params, saved, sink, d_before=None, d_pool0=None, d_pool1=None,
     x, y1, m1, r1, a1, y2, m2, r2 = saved
     dy2, rs2 = K.in_lrelu_bwd(y2, m2, r2, d_before, d_pool0, d_pool1, rowsum=True)
     g, acc = sink.target(W2)
-    K.conv3_wgrad(dy2, [(a1, 0)], g, acc)
+    sink.wgrad(lambda: K.conv3_wgrad(dy2, [(a1, 0)], g, acc), dy2, a1)
     g, acc = sink.target(b2)
     K.bias_grad_rows(rs2, g, acc)
     da1 = torch.empty_like(a1)
@@ -95,7 +123,7 @@ def downconv_bwd(params, saved, sink, d_before=None, d_pool0=None, d_pool1=None,
     dy1, rs1 = K.in_lrelu_bwd(y1, m1, r1, da1, rowsum=True)
     del da1
     g, acc = sink.target(W1)
-    K.conv3_wgrad(dy1, [(x, 0)], g, acc)
+    sink.wgrad(lambda: K.conv3_wgrad(dy1, [(x, 0)], g, acc), dy1, x)
     g, acc = sink.target(b1)
     K.bias_grad_rows(rs1, g, acc)
     if not need_dx:
@@ -124,14 +152,14 @@ def dense_bwd(params, saved, sink, d_h2, need_dx=True, gated=False):
     s = 1.0 / (1.0 - drop_p)
     dpre2 = d_h2 if gated else K.relu_gate_bwd(d_h2, h2, s)
     g, acc = sink.target(W2)
-    K.linear_wgrad(dpre2, [(h1, 0)], g, acc)
+    sink.wgrad(lambda: K.linear_wgrad(dpre2, [(h1, 0)], g, acc), dpre2, h1)
     g, acc = sink.target(b2)
     K.bias_grad(dpre2, g, acc)
     dpre1 = torch.empty_like(h1)
     K.linear_dgrad(dpre2, W2, [(dpre1, 0, h1, s)])
     del dpre2
     g, acc = sink.target(W1)
-    K.linear_wgrad(dpre1, [(audio, 0), (midi, 0)], g, acc)
+    sink.wgrad(lambda: K.linear_wgrad(dpre1, [(audio, 0), (midi, 0)], g, acc), dpre1, audio, midi)
     g, acc = sink.target(b1)
     K.bias_grad(dpre1, g, acc)
     if not need_dx:
@@ -190,7 +218,7 @@ def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_
     dw_pre, rs_w = K.in_lrelu_bwd(w_pre, mw_, rw_, d_w, rowsum=True)
     srcs2 = [(v, 0)] + ([(cond, c_cond)] if cond is not None else [])
     g, acc = sink.target(W2)
-    K.conv3_wgrad(dw_pre, srcs2, g, acc)
+    sink.wgrad(lambda: K.conv3_wgrad(dw_pre, srcs2, g, acc), dw_pre, *(t for t, _ in srcs2))
     g, acc = sink.target(b2)
     K.bias_grad_rows(rs_w, g, acc)
     dv = torch.empty_like(v)
@@ -204,7 +232,7 @@ def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_
     dv_pre, rs_v = K.in_lrelu_bwd(v_pre, mv_, rv_, dv, rowsum=True)
     del dv
     g, acc = sink.target(W1)
-    K.conv3_wgrad(dv_pre, [(u, 0), (res, c_res)], g, acc)
+    sink.wgrad(lambda: K.conv3_wgrad(dv_pre, [(u, 0), (res, c_res)], g, acc), dv_pre, u, res)
     g, acc = sink.target(b1)
     K.bias_grad_rows(rs_v, g, acc)
     du = torch.empty_like(u)
@@ -214,7 +242,7 @@ def upconv_bwd(params, saved, sink, d_w, res_gate=None, res_gate_scale=1.0, dec_
     du_pre, rs_u = K.in_lrelu_bwd(u_pre, mu_, ru_, du, rowsum=True)
     del du
     g, acc = sink.target(Wu)
-    K.convT2_wgrad(dec, du_pre, g, acc)
+    sink.wgrad(lambda: K.convT2_wgrad(dec, du_pre, g, acc), dec, du_pre)
     g, acc = sink.target(bu)
     K.bias_grad_rows(rs_u, g, acc)
     d_dec = torch.empty_like(dec)
@@ -297,7 +325,7 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
     W = P["lastconv.weight"]
     x_dec = st["x_dec"]
     g, acc = sink.target(W)
-    K.convT1_wgrad(x_dec, dypre, g, acc, scale=MBR_SCALE)
+    sink.wgrad(lambda: K.convT1_wgrad(x_dec, dypre, g, acc, scale=MBR_SCALE), x_dec, dypre)
     g, acc = sink.target(P["lastconv.bias"])
     K.bias_grad(dypre, g, acc)
     dx = torch.empty_like(x_dec)
@@ -357,6 +385,7 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
             sink.block_done()
             d_before[i] = None
         grads_in.append(d_pool)
+    sink.join()
     return grads_in[0], grads_in[1], d_cond_in
 
 

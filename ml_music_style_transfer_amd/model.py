@@ -14,6 +14,7 @@ its trainable parameters stored in one flat device buffer (and gradients in a
 parallel flat buffer) so Adam and the data-parallel all-reduce each touch one
 contiguous range.
 """
+import os
 import weakref
 
 import torch
@@ -44,6 +45,13 @@ def slot_view(buf, p):
         d0, d1, k = p.shape
         return buf.view(d0, k, d1).permute(0, 2, 1)
     return buf.view_as(p)
+
+
+# MST_WGRAD_STREAM=1 runs the weight-gradient GEMMs on a side stream (engine.GradSink). Off by
+# default: measured on one box it gained 0.6 % (49.92 -> 49.63 ms/step,
+# profiles/r02/bench_m7_wgrad_stream.txt) -- the GEMMs' losses are per-tile overheads more than
+# tail waves -- while the per-kernel roofline timing stops meaning anything once kernels overlap.
+_WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "0") == "1"
 
 
 def _require_cuda(*ts):
@@ -394,7 +402,13 @@ class PerformanceNet(nn.Module):
                 return None
             o, n = ent
             return slot_view(f["grad"][o:o + n], p)
-        return E.GradSink(flat_grad_of, on_ready)
+        side = None
+        if _WGRAD_STREAM:  # weight-gradient GEMMs on a side stream (engine.GradSink)
+            dev = f["grad"].device if f is not None else torch.device("cuda", torch.cuda.current_device())
+            side = self.__dict__.get("_mst_side")
+            if side is None or side.device != dev:
+                side = self.__dict__["_mst_side"] = torch.cuda.Stream(device=dev)
+        return E.GradSink(flat_grad_of, on_ready, side)
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)

@@ -22,6 +22,11 @@ for what in "$@"; do
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_write.log" 2>&1 ;;
+    pmcaux)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcaux_fetch" -o run -- \
+        python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_fetch.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcaux_write" -o run -- \
+        python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_write.log" 2>&1 ;;
     aux)
       timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
     layers)
