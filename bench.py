@@ -168,6 +168,9 @@ def main():
                     help="skip the config-2 / config-5 legs (STFT, mel, Griffin-Lim, multi-scale loss)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="all-reduce after backward instead of overlapped bucket all-reduces")
+    ap.add_argument("--graph", action="store_true",
+                    help="N=1: replay forward + L1 + backward + Adam as one captured hipGraph "
+                         "(graphs.GraphedTrainStep); the STFT front end stays eager")
     ap.add_argument("--adam-overlap", action="store_true",
                     help="Adam per bucket inside backward on a side stream (train.BackwardAdam) "
                          "instead of one launch in opt.step()")
@@ -221,8 +224,21 @@ def main():
     data = torch.from_numpy(np.concatenate([roll, onoff], 1)).to(dev)  # (B, 256, T) train.py:84-85
 
     comm_on = [True]  # off only for the exposed-communication leg after the timed region
+    gstep = None
+    if args.graph:
+        if world > 1 or args.adam_overlap:
+            raise SystemExit("--graph: single GPU, no --adam-overlap")
+        from ml_music_style_transfer_amd.graphs import GraphedTrainStep
+        gstep = GraphedTrainStep(model, opt, warmup=1)
+
+    graph_on = [True]  # off for the per-launch GEMM timing leg (a replay runs no Python)
 
     def step():
+        if gstep is not None and graph_on[0]:
+            target = spectral.stft_logpow(tgt_audio, hop=HOP)
+            x_audio = spectral.stft_logpow(ref_audio, hop=HOP)
+            split = torch.split(data, 128, dim=1)
+            return gstep(split[0], x_audio, split[1], target)
         opt.zero_grad()
         target = spectral.stft_logpow(tgt_audio, hop=HOP)           # (B, 1025, 252)
         x_audio = spectral.stft_logpow(ref_audio, hop=HOP)          # style reference spec
@@ -262,6 +278,7 @@ def main():
     # roofline leg: per-launch HIP events around every GEMM (fp32 MFMA implicit GEMM) of a few
     # extra steps, on the launch stream; achieved = algorithmic FLOPs / summed kernel time.
     log = []
+    graph_on[0] = False
     K.gemm_timing(log)
     for _ in range(args.kernel_timing_steps):
         step()
@@ -327,8 +344,16 @@ def main():
     }
     if comm is not None:
         out["allreduce"] = comm
+    if gstep is not None:
+        out["config"]["hipgraph"] = True
     if not args.no_aux:
         out["aux"] = aux_legs(world, rank, dev, cpu=not args.no_cpu_baseline)
+        try:  # reference inference call (inference.py:74-91): B = 1, one 4 s chunk
+            from ml_music_style_transfer_amd.graphs import inference_step_times
+            out["aux"]["inference_b1"] = {k: (round(v, 4) if isinstance(v, float) else v)
+                                          for k, v in inference_step_times(model).items()}
+        except Exception as e:  # a report leg must not cost the measured line
+            out["aux"]["inference_b1"] = {"error": repr(e)[:200]}
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
     if world > 1:

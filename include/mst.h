@@ -25,7 +25,8 @@
  *                            model/model.py:40-53,65-69,81-89   InstanceNorm1d + LeakyReLU(0.01) [+ MaxPool1d(2)]
  *   mst_l1_fwd_f32 / _bwd_f32, mst_mse_fwd_f32
  *                            model/train.py:132-135,140,158     nn.L1Loss fwd/bwd, nn.MSELoss (test)
- *   mst_adam_f32 / _ex_f32   model/train.py:188,143             optim.Adam(lr=1e-3)
+ *   mst_adam_f32 / _ex_f32 / _dev_f32
+ *                            model/train.py:188,143             optim.Adam(lr=1e-3)
  *   mst_onoff_f32            preprocessing/preprocess.py:148-155 piano-roll binarise + onset/offset
  */
 #ifndef MST_H
@@ -78,7 +79,9 @@ typedef struct mst_dst {
  *   Y[b][m][t*ostride + ophase] = act( alpha * sum_{c,tap} A(m,c,tap) * X(b, c, a*t + beta + g*tap) + bias[m] )
  * with A(m,c,tap) = A[m*sAm + c*sAc + tap*sAt], X the virtual concat of src[0..1]
  * (zero outside [0, Tv)), t in [0, Tn), GEMM dims M x (B*Tn) x (Ctot*taps).
- * Optional dropout (keep with prob 1-p, scale 1/(1-p)) keyed by (seed, dst index). */
+ * Optional dropout (keep with prob 1-p, scale 1/(1-p)) keyed by (seed, dst index); with seed_dev
+ * set the key's seed is seed + *seed_dev, read on the device (a captured hipGraph advances
+ * *seed_dev itself, so replays draw fresh masks). */
 typedef struct mst_conv_desc {
   int32_t B, M, Tn, Ctot, taps;
   int32_t a, beta, g;        /* input time = a*t + beta + g*tap */
@@ -97,6 +100,7 @@ typedef struct mst_conv_desc {
                                 n > 0 = split-K over n slabs, -1 = stream-K over one residency
                                 wave (512 workgroups), n < -1 = stream-K over -n workgroups */
   int32_t pad_;
+  const uint64_t* seed_dev;  /* nullable */
 } mst_conv_desc;
 
 /* Weight gradient of a conv-like layer:
@@ -181,6 +185,11 @@ int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float 
 int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step,
                     float b2, float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt,
                     int32_t max_blocks, void* stream);
+/* The same update with the step-dependent pair read from device memory: hyper[0] = lr_step,
+ * hyper[1] = bc2_sqrt (2 floats). A captured hipGraph (graphs.GraphedTrainStep) computes them
+ * on the device from its own step counter, so one recorded launch serves every step. */
+int mst_adam_dev_f32(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                     float b2, float one_minus_b1, float one_minus_b2, float eps, void* stream);
 
 /* ---- elementwise helpers ---- */
 int mst_scale_f32(float* x, int64_t n, float s, void* stream);

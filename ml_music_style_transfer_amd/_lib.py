@@ -38,7 +38,8 @@ class MstConvDesc(ctypes.Structure):
                 ("Tv", c_int32), ("A", c_void_p), ("sAm", c_int64), ("sAc", c_int64),
                 ("sAt", c_int64), ("src", MstSrc * 2), ("ostride", c_int32), ("ophase", c_int32),
                 ("dst", MstDst * 2), ("alpha", c_float), ("bias", c_void_p), ("act", c_int32),
-                ("drop_p", c_float), ("seed", c_uint64), ("splitk", c_int32), ("pad_", c_int32)]
+                ("drop_p", c_float), ("seed", c_uint64), ("splitk", c_int32), ("pad_", c_int32),
+                ("seed_dev", c_void_p)]
 
 
 class MstWgradDesc(ctypes.Structure):
@@ -77,6 +78,8 @@ SIGNATURES = {
                                c_float, c_float, c_float, c_float, c_void_p]),
     "mst_adam_ex_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                   c_float, c_float, c_float, c_float, c_float, c_int32, c_void_p]),
+    "mst_adam_dev_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                   c_float, c_float, c_float, c_float, c_void_p]),
     "mst_scale_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
     "mst_fill_f32": (c_int32, [c_void_p, c_int64, c_float, c_void_p]),
     "mst_stft_logpow_f32": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32,

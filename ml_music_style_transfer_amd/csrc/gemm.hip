@@ -81,6 +81,7 @@ struct GP {
   int act;
   float drop_p;
   unsigned long long seed;
+  const unsigned long long* seed_dev;  // nullable: key seed = seed + *seed_dev
   // wgrad epilogue
   float* out;
   long long ldo, ldc, ldt;  // column of (c, tap) = c * ldc + tap * ldt
@@ -129,7 +130,8 @@ __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
     if ((unsigned)ts >= (unsigned)p.yT0) return;
     long long idx = (long long)b * p.yb0 + (long long)m * p.yc0 + ts;
     if (p.drop_p > 0.f) {
-      uint32_t h = mst_hash32(p.seed, (unsigned long long)idx);
+      const unsigned long long sd = p.seed + (p.seed_dev ? *p.seed_dev : 0ull);
+      uint32_t h = mst_hash32(sd, (unsigned long long)idx);
       v = (h >= (uint32_t)(p.drop_p * 4294967296.0f)) ? v * (1.f / (1.f - p.drop_p)) : 0.f;
     }
     if (p.gt0) v = p.gt0[idx] > 0.f ? v * p.gs0 : 0.f;
@@ -830,6 +832,7 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.act = d->act;
   p.drop_p = d->drop_p;
   p.seed = d->seed;
+  p.seed_dev = reinterpret_cast<const unsigned long long*>(d->seed_dev);
   choose_sched(p, d->splitk);
   return MST_OK;
 }

@@ -295,10 +295,17 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const double* __restric
 
 // Adam (torch.optim.Adam, single-tensor formulation): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g^2;
 // p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps). Vectorised 4-wide over the flat buffer.
+// hyper (nullable, device) = {lr/bc1, sqrt(bc2)} overrides the by-value pair: a captured
+// hipGraph replays one launch whose step-dependent factors the graph itself computes.
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    long long n, float lr_step, float b2, float w1,
-                                                   float w2, float eps, float bc2_sqrt) {
+                                                   float w2, float eps, float bc2_sqrt,
+                                                   const float* __restrict__ hyper) {
+  if (hyper) {
+    lr_step = hyper[0];
+    bc2_sqrt = hyper[1];
+  }
   long long n4 = n >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (long long)gridDim.x * blockDim.x) {
@@ -504,7 +511,18 @@ int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, flo
   MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, max_blocks)), dim3(256), 0,
                      (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b2, one_minus_b1,
-                     one_minus_b2, eps, bc2_sqrt);
+                     one_minus_b2, eps, bc2_sqrt, (const float*)nullptr);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int mst_adam_dev_f32(float* p, const float* g, float* m, float* v, int64_t n, const float* hyper,
+                     float b2, float one_minus_b1, float one_minus_b2, float eps, void* stream) {
+  MST_REQUIRE(p && g && m && v && hyper && n > 0);
+  MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, p, g, m, v, (long long)n, 0.f, b2, one_minus_b1,
+                     one_minus_b2, eps, 1.f, hyper);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }

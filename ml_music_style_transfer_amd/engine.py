@@ -29,6 +29,7 @@ import torch
 
 from . import _lib as L
 from . import kernels as K
+from . import ops as _ops  # noqa: F401  (registers torch.ops.mst.*)
 
 LRELU = L.ACT_LRELU
 RELU = L.ACT_RELU
@@ -134,14 +135,15 @@ def downconv_bwd(params, saved, sink, d_before=None, d_pool0=None, d_pool1=None,
 
 
 # ---------------------------------------------------------------- DenseConcat
-def dense_fwd(W1, b1, W2, b2, midi, audio, drop_p=0.0, seed=0):
+def dense_fwd(W1, b1, W2, b2, midi, audio, drop_p=0.0, seed=0, seed_dev=None):
     """DenseConcat.forward (model.py:102-108): cat(audio, midi) -> fc1 -> ReLU -> Dropout
     -> fc2 -> ReLU -> Dropout, computed in NCL (no transposes)."""
     B, _, T = midi.shape
     h1 = _e((B, W1.shape[0], T), midi)
-    K.linear_fwd([(audio, 0), (midi, 0)], W1, b1, h1, act=RELU, drop_p=drop_p, seed=seed)
+    K.linear_fwd([(audio, 0), (midi, 0)], W1, b1, h1, act=RELU, drop_p=drop_p, seed=seed,
+                 seed_dev=seed_dev)
     h2 = _e((B, W2.shape[0], T), midi)
-    K.linear_fwd([(h1, 0)], W2, b2, h2, act=RELU, drop_p=drop_p, seed=seed + 1)
+    K.linear_fwd([(h1, 0)], W2, b2, h2, act=RELU, drop_p=drop_p, seed=seed + 1, seed_dev=seed_dev)
     return h2, (midi, audio, h1, h2, drop_p)
 
 
@@ -263,8 +265,9 @@ DN = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
 UP = ("upconv.weight", "upconv.bias", "conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")
 
 
-def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5):
-    """PerformanceNet.forward (model.py:262-300) as one kernel program."""
+def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5, seed_dev=None):
+    """PerformanceNet.forward (model.py:262-300) as one kernel program. seed_dev (optional
+    int64 device scalar) is added to every dropout seed on the device (hipGraph replays)."""
     enc_m, enc_a, sv_m, sv_a = [], [], [], []
     xm = x_midi
     for i in range(depth):
@@ -276,7 +279,7 @@ def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5):
         xa, before, sv = downconv_fwd(*_pp(P, f"down_convs_audio.{i}", DC), xa, i < depth - 1)
         enc_a.append(before)
         sv_a.append(sv)
-    x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed)
+    x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed, seed_dev)
     conds, sv_o = [], []
     c = cond
     for i in range(3):
@@ -287,7 +290,7 @@ def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5):
     sv_dn, sv_up = [], []
     for i in range(4):
         skip, svd = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
-                              enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1))
+                              enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1), seed_dev)
         cd = conds[i - 1] if i < 2 else None
         x, svu = upconv_fwd(*_pp(P, f"up_convs.{i}", UP), skip, x, cd)
         sv_dn.append(svd)
@@ -399,7 +402,8 @@ class PerformanceNetFunction(torch.autograd.Function):
         seed = module._next_seed() if drop_p > 0 else 0
         xm, xa, cd = (t if t.stride(2) == 1 and t.dtype == torch.float32 else t.float().contiguous()
                       for t in (x_midi, x_audio, cond))
-        y, state = network_fwd(P, xm, xa, cd, drop_p, seed, module.depth)
+        y, state = network_fwd(P, xm, xa, cd, drop_p, seed, module.depth,
+                               module.__dict__.get("_mst_seed_dev") if drop_p > 0 else None)
         ctx.module = module
         ctx.state = state
         return y
@@ -429,26 +433,12 @@ class PerformanceNetFunction(torch.autograd.Function):
                 g_c if need[2] else None) + (None,) * n_params
 
 
-class L1LossFunction(torch.autograd.Function):
-    """nn.L1Loss() (train.py:132): mean |pred - target| on the device."""
-
-    @staticmethod
-    def forward(ctx, pred, target):
-        pred = pred.contiguous()
-        target = target.contiguous()
-        ctx.save_for_backward(pred, target)
-        return K.l1_fwd(pred, target)
-
-    @staticmethod
-    def backward(ctx, g):
-        pred, target = ctx.saved_tensors
-        return K.l1_bwd(pred, target, g.contiguous()), None
-
-
 def l1_loss(pred, target):
-    return L1LossFunction.apply(pred, target)
+    """nn.L1Loss() (train.py:132): mean |pred - target| on the device (torch.ops.mst.l1_loss;
+    its registered backward is mst::l1_loss_backward)."""
+    return torch.ops.mst.l1_loss(pred, target)
 
 
 def mse_loss(pred, target):
-    """nn.MSELoss() forward (test(), train.py:158); evaluation only."""
-    return K.mse_fwd(pred.contiguous(), target.contiguous())
+    """nn.MSELoss() forward (test(), train.py:158); evaluation only (torch.ops.mst.mse_loss)."""
+    return torch.ops.mst.mse_loss(pred, target)

@@ -69,10 +69,33 @@ def _dst(spec):
     return d
 
 
-def _workspace(nbytes, device):
+# Workspace arena: one grow-only scratch buffer per (device, launch stream). Launches on one
+# stream are ordered, so consecutive GEMM / loss / Griffin-Lim launches share it instead of
+# paying an allocator round trip each. A buffer that is outgrown is retired, never freed: a
+# captured hipGraph may still name it. Under stream capture the arena is bypassed and each
+# launch takes a fresh buffer from the graph's private pool (torch's capture semantics).
+_ARENA = {}
+_RETIRED = []
+
+
+def workspace(nbytes, device):
+    """(float32 buffer of >= nbytes, its byte size) for one launch on the current stream."""
     if nbytes == 0:
         return None, 0
-    return torch.empty((nbytes + 3) // 4, device=device, dtype=torch.float32), nbytes
+    n = (nbytes + 3) // 4
+    if torch.cuda.is_current_stream_capturing():
+        return torch.empty(n, device=device, dtype=torch.float32), 4 * n
+    key = (device.index, L.stream().value)
+    buf = _ARENA.get(key)
+    if buf is None or buf.numel() < n:
+        if buf is not None:
+            _RETIRED.append(buf)
+            n = max(n, 2 * buf.numel())
+        buf = _ARENA[key] = torch.empty(n, device=device, dtype=torch.float32)
+    return buf, 4 * buf.numel()
+
+
+_workspace = workspace
 
 
 # Optional per-launch GEMM timing (bench.py's roofline leg): when a list is installed, every
@@ -99,7 +122,8 @@ def _timed(launch, flops, tag, shape=None):
 
 
 def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt, dsts, ostride=1,
-              ophase=0, alpha=1.0, bias=None, act=L.ACT_NONE, drop_p=0.0, seed=0, splitk=0):
+              ophase=0, alpha=1.0, bias=None, act=L.ACT_NONE, drop_p=0.0, seed=0, splitk=0,
+              seed_dev=None):
     lib = _lib()
     d = L.MstConvDesc()
     d.B, d.M, d.Tn, d.taps = B, M, Tn, taps
@@ -117,6 +141,7 @@ def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt
     d.act = act
     d.drop_p = drop_p
     d.seed = seed
+    d.seed_dev = seed_dev.data_ptr() if seed_dev is not None else None
     d.splitk = splitk or _FORCE_SPLITK
     ref = ctypes.byref(d)
     ws, nb = _workspace(lib.mst_conv_fwd_workspace_size(ref), A.device)
@@ -237,11 +262,12 @@ def convT1_wgrad(x, dY, dW, accumulate, scale=1.0):
 
 
 # ------------------------------------------------------- Linear over NCL channels
-def linear_fwd(srcs, W, bias, out, act=L.ACT_NONE, drop_p=0.0, seed=0):
+def linear_fwd(srcs, W, bias, out, act=L.ACT_NONE, drop_p=0.0, seed=0, seed_dev=None):
     B, Cout, T = out.shape
     Cin = W.shape[1]
     conv_like(B=B, M=Cout, Tn=T, srcs=srcs, Tv=T, taps=1, a=1, beta=0, g=0, A=W, sAm=Cin, sAc=1,
-              sAt=1, dsts=[(out, 0, None, 1.0)], bias=bias, act=act, drop_p=drop_p, seed=seed)
+              sAt=1, dsts=[(out, 0, None, 1.0)], bias=bias, act=act, drop_p=drop_p, seed=seed,
+              seed_dev=seed_dev)
 
 
 def linear_dgrad(dY, W, dsts):
@@ -311,7 +337,7 @@ def relu_gate_bwd(d, h, scale):
 def _loss(fn, pred, target):
     lib = _lib()
     n = pred.numel()
-    ws = torch.empty(lib.mst_l1_workspace_size(n) // 4 + 2, device=pred.device, dtype=torch.float32)
+    ws, _ = workspace(lib.mst_l1_workspace_size(n) + 8, pred.device)
     loss = torch.empty((), device=pred.device, dtype=torch.float32)
     L.check(getattr(lib, fn)(L.ptr(pred), L.ptr(target), n, L.ptr(loss), L.ptr(ws), L.stream()), fn)
     return loss
@@ -341,6 +367,13 @@ def adam(p, g, m, v, lr_step, b1, b2, eps, bc2_sqrt, max_blocks=None):
         L.check(_lib().mst_adam_f32(*args, L.stream()), "adam")
     else:
         L.check(_lib().mst_adam_ex_f32(*args, max_blocks, L.stream()), "adam")
+
+
+def adam_dev(p, g, m, v, hyper, b1, b2, eps):
+    """adam() with (lr_step, bc2_sqrt) read from the 2-float device tensor `hyper`."""
+    assert hyper.dtype == torch.float32 and hyper.numel() >= 2 and hyper.is_cuda
+    L.check(_lib().mst_adam_dev_f32(L.ptr(p), L.ptr(g), L.ptr(m), L.ptr(v), p.numel(), L.ptr(hyper),
+                                    b2, 1.0 - b1, 1.0 - b2, eps, L.stream()), "adam_dev")
 
 
 def scale_(x, s):

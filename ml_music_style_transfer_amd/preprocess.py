@@ -13,7 +13,7 @@ import glob
 import numpy as np
 import torch
 
-from . import _lib as L
+from . import ops as _ops  # noqa: F401  (registers torch.ops.mst.*)
 from . import spectral
 
 
@@ -127,9 +127,7 @@ def pianoroll_onoff(roll):
     B, T, P = x.shape
     if P != 128:
         raise ValueError("piano roll must have 128 pitches on the last axis")
-    b = torch.empty_like(x)
-    o = torch.empty_like(x)
-    L.check(L.load().mst_onoff_f32(L.ptr(x), B, T, L.ptr(b), L.ptr(o), L.stream()), "onoff")
+    b, o = torch.ops.mst.onoff(x)
     if single:
         b, o = b[0], o[0]
     return _back(b, kind), _back(o, kind)

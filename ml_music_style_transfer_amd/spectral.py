@@ -5,7 +5,8 @@ window, center=True, reflect padding, n_fft=2048):
   logpow       preprocessing/preprocess.py:47-49   np.log1p(np.abs(librosa.stft(y, 2048, 256))**2)
   melspec      tests/plot_spec.py:20                librosa.feature.melspectrogram (slaney, 128 mels)
   griffinlim   model/inference.py:105-110          librosa.griffinlim(n_iter, momentum=0.99)
-All compute runs in libmst_hip's FFT kernels (fft.hip); inputs/outputs are CUDA tensors.
+All compute runs in libmst_hip's FFT kernels (fft.hip) behind the torch.ops.mst.* custom ops
+(ops.py); inputs/outputs are CUDA tensors.
 """
 import math
 
@@ -13,6 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import ops as _ops  # noqa: F401  (registers torch.ops.mst.*)
 
 N_FFT = 2048
 
@@ -34,38 +36,27 @@ def n_frames(L_samples, hop):
 
 
 def stft_logpow(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
-    """(L,) or (B, L) signal -> (F, T) / (B, F, T) log1p(|STFT|^2)."""
-    return _stft_real("mst_stft_logpow_f32", x, hop, n_fft, pad_mode)
+    """(L,) or (B, L) signal -> (F, T) / (B, F, T) log1p(|STFT|^2) (torch.ops.mst.stft_logpow)."""
+    x, single = _as_batch(_check_signal(x))
+    out = torch.ops.mst.stft_logpow(x, n_fft, hop, _pad_code(pad_mode))
+    return out[0] if single else out
 
 
 def stft_power(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
-    """|STFT|^2, same layout as stft_logpow."""
-    return _stft_real("mst_stft_power_f32", x, hop, n_fft, pad_mode)
+    """|STFT|^2, same layout as stft_logpow (torch.ops.mst.stft_power)."""
+    x, single = _as_batch(_check_signal(x))
+    out = torch.ops.mst.stft_power(x, n_fft, hop, _pad_code(pad_mode))
+    return out[0] if single else out
 
 
 def _pad_code(pad_mode):
     return {"reflect": L.PAD_REFLECT, "constant": L.PAD_CONSTANT}[pad_mode]
 
 
-def _stft_real(fn, x, hop, n_fft, pad_mode):
-    x, single = _as_batch(_check_signal(x))
-    B, Ls = x.shape
-    T = n_frames(Ls, hop)
-    out = torch.empty(B, n_fft // 2 + 1, T, device=x.device, dtype=torch.float32)
-    L.check(getattr(L.load(), fn)(L.ptr(x), B, Ls, n_fft, hop, _pad_code(pad_mode), L.ptr(out),
-                                  L.stream()), fn)
-    return out[0] if single else out
-
-
 def stft_complex(x, hop=256, n_fft=N_FFT, pad_mode="reflect"):
     """Complex STFT, frame-major: (B, T, F) complex64 view of a (B, T, F, 2) buffer."""
     x, single = _as_batch(_check_signal(x))
-    B, Ls = x.shape
-    T = n_frames(Ls, hop)
-    out = torch.empty(B, T, n_fft // 2 + 1, 2, device=x.device, dtype=torch.float32)
-    L.check(L.load().mst_stft_complex_f32(L.ptr(x), B, Ls, n_fft, hop, _pad_code(pad_mode),
-                                          L.ptr(out), L.stream()), "stft_complex")
-    out = torch.view_as_complex(out)
+    out = torch.view_as_complex(torch.ops.mst.stft_complex(x, n_fft, hop, _pad_code(pad_mode)))
     return out[0] if single else out
 
 
@@ -74,10 +65,7 @@ def istft(X, hop=256):
     single = X.dim() == 2
     if single:
         X = X.unsqueeze(0)
-    Xr = torch.view_as_real(X.contiguous()).contiguous()
-    B, T, F, _ = Xr.shape
-    y = torch.empty(B, hop * (T - 1), device=X.device, dtype=torch.float32)
-    L.check(L.load().mst_istft_f32(L.ptr(Xr), B, F, T, hop, L.ptr(y), L.stream()), "istft")
+    y = torch.ops.mst.istft(torch.view_as_real(X.contiguous()).contiguous(), int(hop))
     return y[0] if single else y
 
 
@@ -101,35 +89,14 @@ def _inv_wss(T, hop, n_fft, device):
     return _WSS_CACHE[key]
 
 
-class _ISTFTFunction(torch.autograd.Function):
-    """y = istft(X). The iSTFT is linear; its adjoint is a scaled STFT: with
-    h = g / wss on the kept samples (zeros in the trimmed margins, i.e. center padding with
-    constants), dL/dX[k, f] = (c_f / n_fft) * rfft(w * h[k*hop : k*hop + n_fft])[f],
-    c_f = 1 at f = 0 and n_fft/2, else 2 (irfft's Hermitian weights). Both directions are
-    the fft.hip kernels (mst_istft_f32 / mst_stft_complex_f32)."""
-
-    @staticmethod
-    def forward(ctx, X, hop):
-        ctx.hop, ctx.T, ctx.F = hop, X.shape[1], X.shape[2]
-        return istft(X, hop)
-
-    @staticmethod
-    def backward(ctx, g):
-        n_fft = 2 * (ctx.F - 1)
-        h = (g.contiguous() * _inv_wss(ctx.T, ctx.hop, n_fft, g.device)).contiguous()
-        G = stft_complex(h, hop=ctx.hop, n_fft=n_fft, pad_mode="constant")
-        c = torch.full((ctx.F,), 2.0 / n_fft, device=g.device)
-        c[0] = c[-1] = 1.0 / n_fft
-        return G * c, None
-
-
 def istft_autograd(X, hop=256):
     """Differentiable istft: (B, T, F) complex frame-major -> (B, hop*(T-1))."""
     single = X.dim() == 2
     Xb = (X.unsqueeze(0) if single else X).contiguous()
     if not Xb.is_cuda:
         raise RuntimeError("istft_autograd needs a CUDA tensor")
-    y = _ISTFTFunction.apply(Xb, int(hop))
+    # mst::istft's registered backward is the adjoint (a constant-padded STFT of g / wss)
+    y = torch.ops.mst.istft(torch.view_as_real(Xb), int(hop))
     return y[0] if single else y
 
 
@@ -231,13 +198,8 @@ def _mel_tables(sr, n_fft, n_mels, device):
 def melspectrogram(x, sr, n_fft=N_FFT, hop_length=256, n_mels=128, pad_mode="reflect"):
     """librosa.feature.melspectrogram(y, sr, n_fft, hop_length) (power 2, slaney, 128 mels)."""
     x, single = _as_batch(_check_signal(x))
-    B, Ls = x.shape
-    T = n_frames(Ls, hop_length)
     st, ln, wo, w = _mel_tables(sr, n_fft, n_mels, x.device)
-    out = torch.empty(B, n_mels, T, device=x.device, dtype=torch.float32)
-    L.check(L.load().mst_stft_mel_f32(L.ptr(x), B, Ls, n_fft, hop_length, _pad_code(pad_mode),
-                                      L.ptr(st), L.ptr(ln), L.ptr(wo), L.ptr(w), n_mels, L.ptr(out),
-                                      L.stream()), "stft_mel")
+    out = torch.ops.mst.melspectrogram(x, n_fft, hop_length, _pad_code(pad_mode), st, ln, wo, w)
     return out[0] if single else out
 
 
@@ -269,54 +231,13 @@ def griffinlim(S, n_iter=60, hop_length=256, momentum=0.99, init="random", seed=
         ang = None
     else:
         raise ValueError(f"init={init!r} must be 'random', None or a tensor")
-    lib = L.load()
-    nbytes = lib.mst_griffinlim_workspace_size(B, F, T, hop_length)
-    ws = torch.empty(nbytes // 4 + 64, device=S.device, dtype=torch.float32)
-    y = torch.empty(B, hop_length * (T - 1), device=S.device, dtype=torch.float32)
-    L.check(lib.mst_griffinlim_f32(L.ptr(S), B, F, T, hop_length, n_iter, float(momentum),
-                                   L.ptr(ang), 1 if from_logpow else 0, L.ptr(y), L.ptr(ws),
-                                   ws.numel() * 4, L.stream()), "griffinlim")
+    y = torch.ops.mst.griffinlim(S, int(n_iter), int(hop_length), float(momentum), ang,
+                                 bool(from_logpow))
     return y[0] if single else y
 
 
 # ------------------------------------------------------- multi-scale spectral loss
 MSS_SIZES = (2048, 1024, 512, 256, 128, 64)
-
-
-def _mss_call(pred, target, alpha, eps, sizes, want_grad):
-    import ctypes
-    lib = L.load()
-    B, Ls = pred.shape
-    arr = (ctypes.c_int32 * len(sizes))(*sizes)
-    nbytes = lib.mst_mss_workspace_size(B, Ls, len(sizes), arr)
-    if nbytes == 0:
-        raise ValueError(f"multiscale_spectral_loss: bad sizes {sizes} for length {Ls} "
-                         "(powers of two in [64, 2048], at most 8, signal longer than n/2)")
-    ws = torch.empty(nbytes // 4 + 16, device=pred.device, dtype=torch.float32)
-    loss = torch.empty((), device=pred.device, dtype=torch.float32)
-    d = torch.empty_like(pred) if want_grad else None
-    L.check(lib.mst_mss_loss_f32(L.ptr(pred), L.ptr(target), B, Ls, len(sizes), arr, float(alpha),
-                                 float(eps), L.ptr(loss), L.ptr(d), L.ptr(ws), ws.numel() * 4,
-                                 L.stream()), "mss_loss")
-    return loss, d
-
-
-class _MSSLossFunction(torch.autograd.Function):
-    """Loss and d/d pred come out of one pass over the frames (mss.hip); backward scales."""
-
-    @staticmethod
-    def forward(ctx, pred, target, alpha, eps, sizes):
-        loss, d = _mss_call(pred, target, alpha, eps, sizes, ctx.needs_input_grad[0])
-        ctx.save_for_backward(d if d is not None else loss)
-        ctx.has_grad = d is not None
-        return loss
-
-    @staticmethod
-    def backward(ctx, g):
-        (d,) = ctx.saved_tensors
-        if not ctx.has_grad:
-            return None, None, None, None, None
-        return d * g, None, None, None, None
 
 
 def multiscale_spectral_loss(pred, target, alpha=1.0, eps=1e-7, sizes=MSS_SIZES):
@@ -331,7 +252,10 @@ def multiscale_spectral_loss(pred, target, alpha=1.0, eps=1e-7, sizes=MSS_SIZES)
         raise ValueError("pred and target must have the same shape")
     pred_b, _ = _as_batch(_check_signal(pred))
     tgt_b, _ = _as_batch(_check_signal(target).detach())
-    return _MSSLossFunction.apply(pred_b, tgt_b, float(alpha), float(eps), tuple(int(n) for n in sizes))
+    want = torch.is_grad_enabled() and pred_b.requires_grad
+    loss, _ = torch.ops.mst.mss_loss(pred_b, tgt_b, [int(n) for n in sizes], float(alpha),
+                                     float(eps), want)
+    return loss
 
 
 def spectral_convergence(S, y, hop=256):

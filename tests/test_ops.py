@@ -1,0 +1,152 @@
+"""torch.ops.mst custom ops (ops.py): registration, fake (meta) kernels, autograd wiring.
+
+CPU part: every op exists, shape inference under FakeTensorMode matches the real layout, a
+CPU tensor is refused (no CPU path). GPU part: torch.library.opcheck (schema, fake-vs-real,
+autograd registration) and the differentiable layer ops against torch.nn.functional in
+float64 on the CPU (fp32 GEMM tolerance 2e-5 of the absolute-product scale).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch._subclasses.fake_tensor import FakeTensorMode
+
+from ml_music_style_transfer_amd import ops  # noqa: F401
+
+
+def test_ops_registered():
+    for name in ops.OPS:
+        assert hasattr(torch.ops.mst, name), name
+
+
+def test_fake_shapes():
+    with FakeTensorMode():
+        x = torch.empty(3, 16384, device="cuda")
+        assert torch.ops.mst.stft_logpow(x, 2048, 256, 0).shape == (3, 1025, 65)
+        assert torch.ops.mst.stft_power(x, 1024, 128, 1).shape == (3, 513, 129)
+        X = torch.ops.mst.stft_complex(x, 2048, 256, 0)
+        assert X.shape == (3, 65, 1025, 2)
+        assert torch.ops.mst.istft(X, 256).shape == (3, 16384)
+        st = torch.empty(128, dtype=torch.int32, device="cuda")
+        w = torch.empty(2000, device="cuda")
+        assert torch.ops.mst.melspectrogram(x, 2048, 256, 0, st, st, st, w).shape == (3, 128, 65)
+        S = torch.empty(3, 1025, 65, device="cuda")
+        assert torch.ops.mst.griffinlim(S, 4, 256, 0.99, None, True).shape == (3, 16384)
+        loss, d = torch.ops.mst.mss_loss(x, x, [2048, 512, 64], 1.0, 1e-7, True)
+        assert loss.shape == () and d.shape == x.shape
+        assert torch.ops.mst.mss_loss(x, x, [64], 1.0, 1e-7, False)[1].numel() == 0
+        assert torch.ops.mst.l1_loss(x, x).shape == ()
+        assert torch.ops.mst.l1_loss_backward(x, x, torch.empty((), device="cuda")).shape == x.shape
+        roll = torch.empty(2, 50, 128, device="cuda")
+        b, o = torch.ops.mst.onoff(roll)
+        assert b.shape == o.shape == roll.shape
+        h = torch.empty(2, 64, 100, device="cuda")
+        assert torch.ops.mst.conv1d_k3(h, torch.empty(32, 64, 3, device="cuda"), None).shape == (2, 32, 100)
+        for k, tout in ((2, 198), (3, 199), (4, 200), (6, 202)):
+            W = torch.empty(64, 16, k, device="cuda")
+            assert torch.ops.mst.conv_transpose1d(h, W, None, 2).shape == (2, 16, tout)
+        W = torch.empty(64, 16, 3, device="cuda")
+        assert torch.ops.mst.conv_transpose1d(h, W, None, 1).shape == (2, 16, 100)
+        assert torch.ops.mst.linear_ncl(h, torch.empty(20, 64, device="cuda"), None).shape == (2, 20, 100)
+        dx, dW, db = torch.ops.mst.conv1d_k3_backward(torch.empty(2, 32, 100, device="cuda"), h,
+                                                      torch.empty(32, 64, 3, device="cuda"))
+        assert dx.shape == h.shape and dW.shape == (32, 64, 3) and db.shape == (32,)
+
+
+def test_fake_matches_torch_convtranspose_lengths():
+    # the fake kernel's output length is nn.ConvTranspose1d(k, stride 2, padding 1)'s
+    for k in (2, 3, 4, 6):
+        for Tin in (1, 2, 7, 63):
+            if (Tin - 1) * 2 - 2 + k <= 0:
+                continue
+            ref = F.conv_transpose1d(torch.zeros(1, 1, Tin), torch.zeros(1, 1, k), stride=2, padding=1)
+            with FakeTensorMode():
+                got = torch.ops.mst.conv_transpose1d(torch.empty(1, 1, Tin, device="cuda"),
+                                                     torch.empty(1, 1, k, device="cuda"), None, 2)
+            assert got.shape[2] == ref.shape[2], (k, Tin)
+
+
+def test_convtranspose_unsupported_kernel_refused():
+    with FakeTensorMode(), pytest.raises(ValueError, match="stride 2 with k in"):
+        torch.ops.mst.conv_transpose1d(torch.empty(1, 4, 8, device="cuda"),
+                                       torch.empty(4, 4, 5, device="cuda"), None, 2)
+
+
+def test_cpu_tensor_refused():
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        torch.ops.mst.stft_logpow(torch.zeros(1, 4096), 2048, 256, 0)
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        torch.ops.mst.conv1d_k3(torch.zeros(1, 2, 8), torch.zeros(3, 2, 3), None)
+
+
+# ------------------------------------------------------------------------------ GPU
+def _r(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1
+
+
+@pytest.mark.gpu
+def test_opcheck_spectral(cuda):
+    x = _r(2, 8192, seed=1).float().to(cuda)
+    torch.library.opcheck(torch.ops.mst.stft_logpow, (x, 2048, 256, 0))
+    torch.library.opcheck(torch.ops.mst.stft_power, (x, 2048, 128, 1))
+    torch.library.opcheck(torch.ops.mst.stft_complex, (x, 2048, 256, 0))
+    X = torch.ops.mst.stft_complex(x, 2048, 256, 0).requires_grad_(True)
+    torch.library.opcheck(torch.ops.mst.istft, (X, 256))
+    S = torch.ops.mst.stft_logpow(x, 2048, 256, 0)
+    torch.library.opcheck(torch.ops.mst.griffinlim, (S, 2, 256, 0.99, None, True))
+    p = x.clone().requires_grad_(True)
+    t = _r(2, 8192, seed=2).float().to(cuda)
+    torch.library.opcheck(torch.ops.mst.mss_loss, (p, t, [2048, 256, 64], 1.0, 1e-7, True))
+    torch.library.opcheck(torch.ops.mst.l1_loss, (p, t))
+    torch.library.opcheck(torch.ops.mst.onoff, ((torch.rand(2, 40, 128, device=cuda) > 0.7).float(),))
+
+
+def _check(got, ref, scale, what, rtol=2e-5):
+    err = (got.detach().double().cpu() - ref.detach()).abs().max().item()
+    assert err <= rtol * max(float(scale), 1e-30), f"{what}: {err:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["conv3", "convT2_k4", "convT2_k6", "convT1", "linear"])
+def test_layer_ops_autograd(cuda, kind):
+    B, Cin, Cout, T = 3, 37, 29, 41
+    x = _r(B, Cin, T, seed=3)
+    if kind == "conv3":
+        W = _r(Cout, Cin, 3, seed=4)
+        op = lambda x_, W_, b_: torch.ops.mst.conv1d_k3(x_, W_, b_)  # noqa: E731
+        ref = lambda x_, W_, b_: F.conv1d(x_, W_, b_, padding=1)  # noqa: E731
+    elif kind.startswith("convT2"):
+        k = int(kind[-1])
+        W = _r(Cin, Cout, k, seed=4)
+        op = lambda x_, W_, b_: torch.ops.mst.conv_transpose1d(x_, W_, b_, 2)  # noqa: E731
+        ref = lambda x_, W_, b_: F.conv_transpose1d(x_, W_, b_, stride=2, padding=1)  # noqa: E731
+    elif kind == "convT1":
+        W = _r(Cin, Cout, 3, seed=4)
+        op = lambda x_, W_, b_: torch.ops.mst.conv_transpose1d(x_, W_, b_, 1)  # noqa: E731
+        ref = lambda x_, W_, b_: F.conv_transpose1d(x_, W_, b_, stride=1, padding=1)  # noqa: E731
+    else:
+        W = _r(Cout, Cin, seed=4)
+        op = lambda x_, W_, b_: torch.ops.mst.linear_ncl(x_, W_, b_)  # noqa: E731
+        ref = lambda x_, W_, b_: F.linear(x_.transpose(1, 2), W_, b_).transpose(1, 2)  # noqa: E731
+    b = _r(Cout, seed=5)
+    xr, Wr, br = (t.clone().requires_grad_(True) for t in (x, W, b))
+    yr = ref(xr, Wr, br)
+    dy = _r(*yr.shape, seed=6)
+    yr.backward(dy)
+    xg, Wg, bg = (t.float().to(cuda).requires_grad_(True) for t in (x, W, b))
+    y = op(xg, Wg, bg)
+    assert y.shape == yr.shape
+    y.backward(dy.float().to(cuda))
+    taps = W.shape[2] if W.dim() == 3 else 1
+    _check(y, yr, Cin * taps, f"{kind} fwd")
+    _check(xg.grad, xr.grad, Cout * taps, f"{kind} dx")
+    _check(Wg.grad, Wr.grad, B * T * 2, f"{kind} dW")
+    _check(bg.grad, br.grad, B * T * 2, f"{kind} db")
+    torch.library.opcheck(torch.ops.mst.conv1d_k3 if kind == "conv3" else
+                          torch.ops.mst.linear_ncl if kind == "linear" else
+                          torch.ops.mst.conv_transpose1d,
+                          (xg.detach().requires_grad_(True), Wg.detach().requires_grad_(True),
+                           bg.detach().requires_grad_(True))
+                          + ((2 if kind.startswith("convT2") else 1,) if kind.startswith("convT") else ()),
+                          test_utils=("test_schema", "test_faketensor",
+                                      "test_autograd_registration"))
