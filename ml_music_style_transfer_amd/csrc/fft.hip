@@ -436,7 +436,6 @@ __global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ 
 // trip per frame instead of three, twiddles from tables instead of product trees, and
 // log1p(p) = log(1 + p) on the hardware log (absolute error <= 1e-6, inside the 1e-4 bar).
 // ---------------------------------------------------------------------------
-constexpr int FPW = 16;            // frames per workgroup (max)
 #ifndef FM_WAVES
 #define FM_WAVES 8                 // frequency-major STFT: waves per workgroup (8 or 16)
 #endif
@@ -540,6 +539,44 @@ __device__ __forceinline__ void fft1024_v2(c2 v[16], c2* S, const FftTabs& tb, i
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   dft16<false>(v);  // Z[lane + 64 q_hi] in v[q_hi]
+}
+
+
+// fft1024_v2 with the twiddles formed from two values: w1 = W1024^lane (stage A, powers by
+// twiddle_powers' depth-4 product tree) and wb = W64^(lane & 15) (stage B1, wb^2, wb^3): a
+// caller that keeps no table in LDS issues two loads early instead of eighteen on the FFT's
+// critical path (error: a few ulp per twiddle).
+__device__ __forceinline__ void fft1024_v2p(c2 v[16], c2* S, c2 w1, c2 wb, int lane) {
+  dft16<false>(v);
+  twiddle_powers(v, w1);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) swap32(v[r], v[r + 8]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if ((r & 4) == 0) swap16(v[r], v[r + 4]);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) dft4<false>(v[a], v[a + 4], v[a + 8], v[a + 12]);
+  const int llo = lane & 15, c = lane >> 4;
+  const c2 wb2 = cmul(wb, wb), wb3 = cmul(wb2, wb);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    v[a + 4] = cmul(v[a + 4], wb);
+    v[a + 8] = cmul(v[a + 8], wb2);
+    v[a + 12] = cmul(v[a + 12], wb3);
+  }
+  c2* Sw = S + 68 * c + llo;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) Sw[17 * (a + 16 * q)] = v[a + 4 * q];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const c2* Sr = S + 17 * lane;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = Sr[i];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  dft16<false>(v);
 }
 
 __device__ __forceinline__ float bperm(int src_byte, float x) {
@@ -1247,6 +1284,254 @@ __global__ __launch_bounds__(256) void ola_kernel(const float* __restrict__ fram
   }
 }
 
+// ---------------------------------------------------------------------------
+// Griffin-Lim synthesis in one pass (round 2): spectra -> signal without the frames workspace.
+// The two-pass iSTFT above moves every windowed frame through HBM twice (written by
+// ifft_frames_kernel, read back by ola_kernel: 1 GB per iteration at config 2, on top of the
+// 1.3 GB of spectra), and the fused istft_kernel recomputes 7 halo frames per 32. Here a
+// workgroup (8 waves) owns G consecutive frames of one clip and every sample they cover
+// (<= 8192, 16 per thread, in registers):
+//   per round of 8 frames, wave w: bins of frame f = X = mag * normalise(cur - beta prev)
+//     (issued one round ahead, during the previous round's overlap-add), staged in the wave's
+//     LDS scratch for the irfft pre-twist (bins k and 1024 - k live in different lanes), the
+//     inverse 1024-point FFT as conj(fft1024_v2(conj v))
+//     (tables from global memory: the LDS holds the 8 frames), window and 1/1024 into the
+//     wave's LDS scratch; barrier; every thread adds the round's frames covering its samples
+//     in increasing frame order.
+//   end: samples whose covering frames all belong to the workgroup are final (divided by the
+//     window-sum-square); the NFFT - hop samples shared with a neighbour (a "seam") go out as
+//     partial sums, and gl_seam_kernel adds the two halves (earlier frames first) and divides.
+// Reads each bin once (20 B: cur, prev, mag), writes each sample once.
+// ---------------------------------------------------------------------------
+constexpr int GLW = 8;                      // waves per synthesis workgroup
+constexpr int GL_OWN = 16;                  // samples per thread
+constexpr int GL_SEG = 64 * GLW * GL_OWN;   // samples a workgroup covers (8192)
+
+// frames per workgroup: the covered span (G - 1) hop + NFFT fits GL_SEG; whole rounds when G >= 8
+static inline int gl_frames(int hop) {
+  const int g = (GL_SEG - NFFT) / hop + 1;
+  return g >= GLW ? g / GLW * GLW : g;
+}
+
+// Squared periodic Hann, sin^4(pi n / 2048) (the sin^2 form of the synthesis window), into an
+// LDS table: computed, not looked up, so no load latency sits at the start of a workgroup.
+__device__ __forceinline__ void gl_fill_h2(float* h2) {
+  for (int n = threadIdx.x; n < NFFT; n += blockDim.x) {
+    const float sn = sinpif((float)n * (1.f / NFFT));
+    h2[n] = (sn * sn) * (sn * sn);
+  }
+}
+
+// window-sum-square at padded sample sp, frames in increasing order
+__device__ __forceinline__ float gl_wss(const float* h2, int sp, int fmin, int fmax, int hop) {
+  float s = 0.f;
+  for (int fr = fmin; fr <= fmax; ++fr) s += h2[sp - fr * hop];
+  return s;
+}
+
+// One frame's raw bins in registers (issued a round ahead, consumed by gl_frame_x).
+struct GlRaw {
+  float2 c[17], p[17];
+};
+
+__device__ __forceinline__ float2 gl_ld2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// Issue frame f's bin loads (k = lane + 64 j, and bin 1024 in every lane as entry 16). Always
+// issued (a frame past the workgroup's range reads zeros through an empty descriptor): a
+// conditional refill would keep the previous values live across the FFT.
+__device__ __forceinline__ void gl_issue(const float2* cur, const float2* prev, int b, int T,
+                                         int f, bool valid, int lane, GlRaw& r) {
+  const long long base = ((long long)b * T + (valid ? f : 0)) * NB;
+  // absent operands (cur == NULL: all-ones phases; prev == NULL: no momentum) read zeros too
+  const auto rc = frame_rsrc(cur ? cur + base : nullptr, valid && cur ? NB * 8 : 0);
+  const auto rp = frame_rsrc(prev ? prev + base : nullptr, valid && prev ? NB * 8 : 0);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) r.c[j] = gl_ld2(rc, lane * 8, 64 * j * 8);
+  r.c[16] = gl_ld2(rc, 0, NC * 8);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) r.p[j] = gl_ld2(rp, lane * 8, 64 * j * 8);
+  r.p[16] = gl_ld2(rp, 0, NC * 8);
+}
+
+// frame f's magnitudes (loaded when the frame is synthesised, not a round ahead: registers)
+__device__ __forceinline__ float gl_mag(__amdgpu_buffer_rsrc_t rm, int lane, int j) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rm, j < 16 ? lane * 4 : 0,
+                                                                        j < 16 ? 64 * j * 4 : NC * 4, 0));
+}
+
+// X = mag * normalise(cur - beta prev) (gl_bin's arithmetic) for entry j
+__device__ __forceinline__ c2 gl_x(const GlRaw& r, float mg, int j, bool has_c, bool has_p,
+                                   bool norm, float beta) {
+  c2 a = has_c ? mk(r.c[j].x, r.c[j].y) : mk(1.f, 0.f);
+  if (has_p) a = a - mk(r.p[j].x, r.p[j].y) * beta;
+  if (norm) {
+    const float inv = __builtin_amdgcn_rcpf(__builtin_amdgcn_sqrtf(a.x * a.x + a.y * a.y) + 1e-16f);
+    a = mk(a.x * inv, a.y * inv);
+  }
+  return a * mg;
+}
+
+// LDS-only workgroup barrier: __syncthreads() would also drain vmcnt, i.e. wait for the next
+// round's bin loads issued just before the overlap-add
+#define GL_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+__global__ __launch_bounds__(512, 4) void gl_synth_kernel(const float2* __restrict__ cur,
+                                                          const float2* __restrict__ prev,
+                                                          const float* __restrict__ mag,
+                                                          float beta, int normalize, int T,
+                                                          int hop, int G, int nwg,
+                                                          float* __restrict__ y,
+                                                          float* __restrict__ seamL,
+                                                          float* __restrict__ seamR) {
+  __shared__ __attribute__((aligned(16))) c2 scratch[GLW * SCR];
+  __shared__ float h2[NFFT];
+  const int b = blockIdx.y, wg = blockIdx.x;
+  const int F0 = wg * G, F1 = min(T, F0 + G);
+  const int L = hop * (T - 1);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  gl_fill_h2(h2);  // read after the loop's barriers
+  c2* S = scratch + wave * SCR;
+  const float* Sf = reinterpret_cast<const float*>(scratch);
+  const int c0 = F0 * hop;  // padded coordinate of the first covered sample
+  float acc[GL_OWN];
+#pragma unroll
+  for (int i = 0; i < GL_OWN; ++i) acc[i] = 0.f;
+  const float inv_hop = 1.f / (float)hop;
+  const bool has_c = cur != nullptr, has_p = prev != nullptr, norm = normalize != 0;
+  c2 eh;  // W4096^(2 lane + 1): the window phase of the odd samples
+  {
+    double sn, cs;
+    sincospi((2.0 * (threadIdx.x & 63) + 1.0) / 2048.0, &sn, &cs);
+    eh = mk((float)cs, (float)-sn);
+  }
+  GlRaw rb;
+  gl_issue(cur, prev, b, T, F0 + wave, F0 + wave < F1, threadIdx.x & 63, rb);
+#pragma unroll 1
+  for (int fb = F0; fb < F1; fb += GLW) {
+    const int f = fb + wave;
+    if (f < F1) {
+      int tid = threadIdx.x;
+      __asm__ volatile("" : "+v"(tid));  // lane values formed here, not hoisted out of the loop
+      const int lane = tid & 63;
+      const float2 e1f = kFftTabs.p[lane], wbf = kFftTabs.p[32 * (lane & 15)];  // W2048^lane, W64^(lane & 15)
+      const auto rm = frame_rsrc(mag + ((long long)b * T + f) * NB, NB * 4);
+      float mg[17];
+#pragma unroll
+      for (int j = 0; j < 17; ++j) mg[j] = gl_mag(rm, lane, j);
+      // X staged in the wave's scratch (each bin formed once; the pre-twist pairs k with
+      // 1024 - k, which live in different lanes)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) S[lane + 64 * j] = gl_x(rb, mg[j], j, has_c, has_p, norm, beta);
+      if (lane == 0) S[NC] = gl_x(rb, mg[16], 16, has_c, has_p, norm, beta);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const c2 e1 = mk(e1f.x, e1f.y);
+      // irfft pre-twist: v[k] = Xe + i Xo, Xe = (X_k + conj X_{1024-k}) / 2,
+      // Xo = (X_k - conj X_{1024-k}) conj(W2048^k) / 2
+      c2 V[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int k = lane + 64 * j;
+        c2 Xk = S[k];
+        c2 Xn = S[NC - k];
+        if (k == 0) {  // irfft ignores the imaginary parts of DC and Nyquist
+          Xk.y = 0.f;
+          Xn.y = 0.f;
+        }
+        const c2 Xc = conj(Xn);
+        const c2 xe = (Xk + Xc) * 0.5f;
+        const c2 xo = cmul(Xk - Xc, conj(tw_bin(e1, j))) * 0.5f;
+        const c2 v = xe + mk(-xo.y, xo.x);
+        V[j] = conj(v);  // inverse FFT = conj(FFT(conj v))
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();  // every lane has read the bins before the FFT reuses S
+      fft1024_v2p(V, S, cmul(e1, e1), mk(wbf.x, wbf.y), lane);
+      const float scale = 1.f / NC;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {  // z[n] = conj(V[j]), n = lane + 64 j: samples 2n, 2n + 1
+        const c2 u = V[j];
+        S[lane + 64 * j] = mk(u.x * (hann_sq(e1, j) * scale), -u.y * (hann_sq(eh, j) * scale));
+      }
+    }
+    GL_BARRIER();
+    // the next round's bins are in flight during the overlap-add below
+    gl_issue(cur, prev, b, T, fb + GLW + wave, fb + GLW + wave < F1, threadIdx.x & 63, rb);
+    const int fe = min(fb + GLW, F1) - 1;
+    int zero;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+    // frame-stationary: for each of the round's frames (in increasing order) and each block of
+    // the wave's 64 samples, a wave-uniform test on the block's offset m0 in the frame: fully
+    // inside adds without a per-lane check, partly inside with one, outside skips
+    const int wbase = c0 + 64 * wave;
+    const int lane4 = (threadIdx.x & 63) + zero;
+    for (int fr = fb; fr <= fe; ++fr) {
+      const float* Fr = Sf + (fr - fb) * (2 * SCR) + lane4;
+      const int m00 = wbase - fr * hop;
+#pragma unroll
+      for (int i = 0; i < GL_OWN; ++i) {
+        const int m0 = m00 + 512 * i;  // wave-uniform
+        if (m0 + 63 < 0 || m0 >= NFFT) continue;
+        if (m0 >= 0 && m0 + 63 < NFFT) {
+          acc[i] += Fr[m0];
+        } else {
+          const int m = m0 + lane4;
+          if ((unsigned)m < (unsigned)NFFT) acc[i] += Fr[m0];
+        }
+      }
+    }
+    GL_BARRIER();
+  }
+  const int cov_end = (F1 - 1) * hop + NFFT;
+  float* yr = y + (long long)b * L;
+  const long long seam0 = (long long)b * (nwg - 1);
+#pragma unroll
+  for (int i = 0; i < GL_OWN; ++i) {
+    const int sp = c0 + threadIdx.x + 512 * i;
+    if (sp >= cov_end) continue;
+    const int fmin = (sp - NFFT) >= 0 ? div_hop(sp - NFFT, hop, inv_hop) + 1 : 0;
+    const int fmax = min(div_hop(sp, hop, inv_hop), T - 1);
+    if (F0 > 0 && fmin < F0) {  // shared with the previous workgroup (its right seam)
+      seamL[(seam0 + wg - 1) * NFFT + (sp - c0)] = acc[i];
+      continue;
+    }
+    if (F1 < T && fmax >= F1) {  // shared with the next workgroup
+      seamR[(seam0 + wg) * NFFT + (sp - F1 * hop)] = acc[i];
+      continue;
+    }
+    const int s = sp - NFFT / 2;
+    if (s < 0 || s >= L) continue;
+    const float wss = gl_wss(h2, sp, fmin, fmax, hop);
+    yr[s] = wss > 1.17549435e-38f ? acc[i] * __builtin_amdgcn_rcpf(wss) : acc[i];
+  }
+}
+
+// The NFFT - hop samples of every seam j of clip b (between synthesis workgroups j and j + 1):
+// left partial (frames of workgroup j) + right partial, then / wss. One workgroup per clip
+// (the Hann^2 table is built once per clip, not once per seam).
+__global__ __launch_bounds__(512) void gl_seam_kernel(const float* __restrict__ seamL,
+                                                      const float* __restrict__ seamR, int T,
+                                                      int hop, int G, int nwg,
+                                                      float* __restrict__ y) {
+  __shared__ float h2[NFFT];
+  gl_fill_h2(h2);
+  __syncthreads();
+  const int b = blockIdx.x;
+  const int L = hop * (T - 1), W = NFFT - hop;
+  const long long o = (long long)b * (nwg - 1) * NFFT;
+  for (int e = threadIdx.x; e < (nwg - 1) * W; e += blockDim.x) {
+    const int j = e / W, m = e - j * W;
+    const int sp = (j + 1) * G * hop + m, s = sp - NFFT / 2;
+    if (s < 0 || s >= L) continue;
+    const float acc = seamR[o + (long long)j * NFFT + m] + seamL[o + (long long)j * NFFT + m];
+    const int fmin = (sp - NFFT) >= 0 ? (sp - NFFT) / hop + 1 : 0;
+    const float wss = gl_wss(h2, sp, fmin, min(sp / hop, T - 1), hop);
+    y[(long long)b * L + s] = wss > 1.17549435e-38f ? acc * __builtin_amdgcn_rcpf(wss) : acc;
+  }
+}
+
 // (B, F, T) -> (B, T, F) with optional log-power -> magnitude (inference.py:109).
 __global__ void transpose_mag_kernel(const float* __restrict__ S, int F, int T, int mag_from_logpow,
                                      float* __restrict__ St) {
@@ -1328,6 +1613,35 @@ int istft2_launch(const float2* cur, const float2* prev, const float* mag, float
   return MST_OK;
 }
 
+// One-pass Griffin-Lim synthesis (gl_synth_kernel + gl_seam_kernel); seams: B (nwg - 1) NFFT
+// floats each for the left and right partial sums.
+static bool gl_one_pass(int hop) {
+  static const bool two = [] {  // MST_GL_TWO_PASS=1: the frames-workspace path (A/B tuning)
+    const char* e = getenv("MST_GL_TWO_PASS");
+    return e && e[0] == '1';
+  }();
+  return !two && hop <= 1024;
+}
+
+int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, float beta,
+                    int normalize, int B, int T, int hop, float* seamL, float* seamR, float* y,
+                    hipStream_t st) {
+  const int G = gl_frames(hop);
+  const int nwg = ceil_div(T, G);
+  hipLaunchKernelGGL(gl_synth_kernel, dim3(nwg, B), dim3(64 * GLW), 0, st, cur, prev, mag, beta,
+                     normalize, T, hop, G, nwg, y, seamL, seamR);
+  MST_CHECK_LAUNCH();
+  if (nwg > 1) {
+    hipLaunchKernelGGL(gl_seam_kernel, dim3(B), dim3(512), 0, st, seamL, seamR, T, hop, G, nwg, y);
+    MST_CHECK_LAUNCH();
+  }
+  return MST_OK;
+}
+
+static size_t gl_seam_floats(int B, int T, int hop) {
+  return (size_t)B * (ceil_div(T, gl_frames(hop)) - 1) * NFFT;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1386,7 +1700,8 @@ size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t ho
   // St (real, all clips) + two complex spectra + signal + windowed frames of one chunk, each
   // rounded to 256 B
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
-  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4);
+  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4) +
+         2 * r(gl_seam_floats(CB, T, hop) * 4);
 }
 
 int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
@@ -1407,12 +1722,19 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   float* sig = (float*)(w + r(bins * 4) + 2 * r(cbins * 8));
   const int L = hop * (T - 1);
   float* frames = (float*)(w + r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4));
+  float* seamL = (float*)((char*)frames + r((size_t)CB * T * NFFT * 4));
+  float* seamR = (float*)((char*)seamL + r(gl_seam_floats(CB, T, hop) * 4));
+  const bool one = gl_one_pass(hop);
+  const float beta = momentum / (1.f + momentum);
+  auto synth = [&](const float2* c, const float2* p, const float* m, int nb, float* out) {
+    return one ? gl_synth_launch(c, p, m, beta, c != nullptr, nb, T, hop, seamL, seamR, out, st)
+               : istft2_launch(c, p, m, beta, c != nullptr, nb, T, hop, frames, out, st);
+  };
   {
     dim3 grid(ceil_div(T, 32), ceil_div(F, 32), B), block(32, 8);
     hipLaunchKernelGGL(transpose_mag_kernel, grid, block, 0, st, S, F, T, mag_from_logpow, St);
     MST_CHECK_LAUNCH();
   }
-  const float beta = momentum / (1.f + momentum);
   for (int c0 = 0; c0 < B; c0 += CB) {
     const int nb = min(CB, B - c0);
     const float* Sc = St + (size_t)c0 * F * T;
@@ -1423,7 +1745,7 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
     float2* bufs[2] = {R0, R1};
     int rc;
     for (int it = 0; it < n_iter; ++it) {
-      rc = istft2_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, frames, sig, st);
+      rc = synth(cur, prev, Sc, nb, sig);
       if (rc) return rc;
       float2* nxt = bufs[it & 1];
       rc = stft_launch(MODE_COMPLEX, sig, nb, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
@@ -1431,8 +1753,7 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
       prev = (it == 0) ? nullptr : cur;
       cur = nxt;
     }
-    rc = istft2_launch(cur, prev, Sc, beta, cur != nullptr, nb, T, hop, frames, y + (size_t)c0 * L,
-                       st);
+    rc = synth(cur, prev, Sc, nb, y + (size_t)c0 * L);
     if (rc) return rc;
   }
   return MST_OK;

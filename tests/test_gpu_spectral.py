@@ -113,6 +113,26 @@ def test_griffinlim_vs_oracle(cuda):
     assert audio.shape == (256 * (T - 1),) and np.isfinite(audio).all()
 
 
+@pytest.mark.parametrize("hop,T", [(256, 6), (256, 24), (256, 25), (256, 49), (64, 200),
+                                   (128, 97), (512, 30), (1024, 15), (768, 20)])
+def test_griffinlim_synthesis_hops(cuda, hop, T):
+    """The one-pass synthesis (gl_synth_kernel: workgroups of G frames, seams between them)
+    across hops and frame counts: one workgroup, a last workgroup of one frame, several seams,
+    hops that do not divide n_fft (no window-sum-square table)."""
+    from ml_music_style_transfer_amd import spectral
+    x = _piano(hop * (T - 1), 16000, 30 + T)
+    S = np.abs(SR.stft(x, hop=hop, out_dtype=None)).astype(np.float32)
+    rng = np.random.RandomState(T)
+    ang = np.exp(2j * np.pi * rng.rand(T, S.shape[0])).astype(np.complex64)
+    ang_t = torch.view_as_real(torch.from_numpy(ang)).contiguous().to(cuda)[None]
+    for n_iter in (0, 2):
+        y = spectral.griffinlim(torch.from_numpy(S).to(cuda), n_iter=n_iter, hop_length=hop,
+                                init=ang_t).cpu().numpy()
+        y_ref = SR.griffinlim(S, n_iter=n_iter, hop=hop, angles=ang.T)
+        assert y.shape == y_ref.shape
+        assert np.abs(y - y_ref).max() <= 1e-4 * np.abs(y_ref).max() + 1e-6, (hop, T, n_iter)
+
+
 def test_griffinlim_clip_chunks(cuda):
     """Griffin-Lim runs in clip chunks of at most 2 GB of workspace: at T = 36000 frames
     (~1.07 GB per clip) a chunk is one clip, so B = 3 runs three chunks; each clip must equal
