@@ -1294,13 +1294,15 @@ __global__ __launch_bounds__(256) void ola_kernel(const float* __restrict__ fram
 //   per round of 8 frames, wave w: bins of frame f = X = mag * normalise(cur - beta prev)
 //     (issued one round ahead, during the previous round's overlap-add), staged in the wave's
 //     LDS scratch for the irfft pre-twist (bins k and 1024 - k live in different lanes), the
-//     inverse 1024-point FFT as conj(fft1024_v2(conj v))
-//     (tables from global memory: the LDS holds the 8 frames), window and 1/1024 into the
+//     inverse 1024-point FFT as conj(fft1024_v2p(conj v))
+//     (twiddles from two table values: the LDS holds the 8 frames), window and 1/1024 into the
 //     wave's LDS scratch; barrier; every thread adds the round's frames covering its samples
 //     in increasing frame order.
 //   end: samples whose covering frames all belong to the workgroup are final (divided by the
 //     window-sum-square); the NFFT - hop samples shared with a neighbour (a "seam") go out as
 //     partial sums, and gl_seam_kernel adds the two halves (earlier frames first) and divides.
+//     (Finishing a seam in whichever workgroup arrives second needs a device-scope release /
+//     acquire: on gfx950 that writes back the XCD's L2, and the kernel ran 8x slower.)
 // Reads each bin once (20 B: cur, prev, mag), writes each sample once.
 // ---------------------------------------------------------------------------
 constexpr int GLW = 8;                      // waves per synthesis workgroup
@@ -1508,27 +1510,50 @@ __global__ __launch_bounds__(512, 4) void gl_synth_kernel(const float2* __restri
   }
 }
 
-// The NFFT - hop samples of every seam j of clip b (between synthesis workgroups j and j + 1):
-// left partial (frames of workgroup j) + right partial, then / wss. One workgroup per clip
-// (the Hann^2 table is built once per clip, not once per seam).
-__global__ __launch_bounds__(512) void gl_seam_kernel(const float* __restrict__ seamL,
-                                                      const float* __restrict__ seamR, int T,
-                                                      int hop, int G, int nwg,
-                                                      float* __restrict__ y) {
+// Hann^2 (2048) and, when hop divides NFFT, the interior window-sum-square by sample phase
+// (hop entries, frames summed in increasing order): built once per Griffin-Lim call.
+__global__ __launch_bounds__(256) void gl_tables_kernel(int hop, float* __restrict__ h2g,
+                                                        float* __restrict__ wssr) {
   __shared__ float h2[NFFT];
   gl_fill_h2(h2);
   __syncthreads();
-  const int b = blockIdx.x;
-  const int L = hop * (T - 1), W = NFFT - hop;
-  const long long o = (long long)b * (nwg - 1) * NFFT;
-  for (int e = threadIdx.x; e < (nwg - 1) * W; e += blockDim.x) {
-    const int j = e / W, m = e - j * W;
-    const int sp = (j + 1) * G * hop + m, s = sp - NFFT / 2;
+  for (int n = threadIdx.x; n < NFFT; n += blockDim.x) h2g[n] = h2[n];
+  if (NFFT % hop == 0)
+    for (int r = threadIdx.x; r < hop; r += blockDim.x) {
+      float s = 0.f;
+      for (int k = NFFT / hop - 1; k >= 0; --k) s += h2[r + hop * k];
+      wssr[r] = s;
+    }
+}
+
+// The NFFT - hop samples of seam j of clip b (between synthesis workgroups j and j + 1): right
+// partial (frames of workgroup j) + left partial, then / wss.
+__global__ __launch_bounds__(256) void gl_seam_kernel(const float* __restrict__ seamL,
+                                                      const float* __restrict__ seamR, int T,
+                                                      int hop, int G, int nwg,
+                                                      const float* __restrict__ h2g,
+                                                      const float* __restrict__ wssr,
+                                                      float* __restrict__ y) {
+  const int b = blockIdx.y, j = blockIdx.x;
+  const int L = hop * (T - 1);
+  const int base = (j + 1) * G * hop;  // padded coordinate of the seam's first sample
+  const long long o = ((long long)b * (nwg - 1) + j) * NFFT;
+  const bool table = NFFT % hop == 0;
+  for (int m = threadIdx.x; m < NFFT - hop; m += blockDim.x) {
+    const int sp = base + m, s = sp - NFFT / 2;
     if (s < 0 || s >= L) continue;
-    const float acc = seamR[o + (long long)j * NFFT + m] + seamL[o + (long long)j * NFFT + m];
+    const float a = seamR[o + m] + seamL[o + m];
+    const int q = sp / hop;
     const int fmin = (sp - NFFT) >= 0 ? (sp - NFFT) / hop + 1 : 0;
-    const float wss = gl_wss(h2, sp, fmin, min(sp / hop, T - 1), hop);
-    y[(long long)b * L + s] = wss > 1.17549435e-38f ? acc * __builtin_amdgcn_rcpf(wss) : acc;
+    const int fmax = min(q, T - 1);
+    float wss;
+    if (table && fmin == q - NFFT / hop + 1 && fmax == q) {
+      wss = wssr[sp - q * hop];
+    } else {
+      wss = 0.f;
+      for (int fr = fmin; fr <= fmax; ++fr) wss += h2g[sp - fr * hop];
+    }
+    y[(long long)b * L + s] = wss > 1.17549435e-38f ? a * __builtin_amdgcn_rcpf(wss) : a;
   }
 }
 
@@ -1614,7 +1639,7 @@ int istft2_launch(const float2* cur, const float2* prev, const float* mag, float
 }
 
 // One-pass Griffin-Lim synthesis (gl_synth_kernel + gl_seam_kernel); seams: B (nwg - 1) NFFT
-// floats each for the left and right partial sums.
+// floats each for the left and right partial sums; tables: Hann^2 and the interior wss.
 static bool gl_one_pass(int hop) {
   static const bool two = [] {  // MST_GL_TWO_PASS=1: the frames-workspace path (A/B tuning)
     const char* e = getenv("MST_GL_TWO_PASS");
@@ -1624,15 +1649,16 @@ static bool gl_one_pass(int hop) {
 }
 
 int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, float beta,
-                    int normalize, int B, int T, int hop, float* seamL, float* seamR, float* y,
-                    hipStream_t st) {
+                    int normalize, int B, int T, int hop, float* seamL, float* seamR,
+                    const float* tabs, float* y, hipStream_t st) {
   const int G = gl_frames(hop);
   const int nwg = ceil_div(T, G);
   hipLaunchKernelGGL(gl_synth_kernel, dim3(nwg, B), dim3(64 * GLW), 0, st, cur, prev, mag, beta,
                      normalize, T, hop, G, nwg, y, seamL, seamR);
   MST_CHECK_LAUNCH();
   if (nwg > 1) {
-    hipLaunchKernelGGL(gl_seam_kernel, dim3(B), dim3(512), 0, st, seamL, seamR, T, hop, G, nwg, y);
+    hipLaunchKernelGGL(gl_seam_kernel, dim3(nwg - 1, B), dim3(256), 0, st, seamL, seamR, T, hop, G,
+                       nwg, tabs, tabs + NFFT, y);
     MST_CHECK_LAUNCH();
   }
   return MST_OK;
@@ -1701,7 +1727,7 @@ size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t ho
   // rounded to 256 B
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
   return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4) +
-         2 * r(gl_seam_floats(CB, T, hop) * 4);
+         2 * r(gl_seam_floats(CB, T, hop) * 4) + r((NFFT + 1024) * 4);
 }
 
 int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
@@ -1724,10 +1750,15 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   float* frames = (float*)(w + r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4));
   float* seamL = (float*)((char*)frames + r((size_t)CB * T * NFFT * 4));
   float* seamR = (float*)((char*)seamL + r(gl_seam_floats(CB, T, hop) * 4));
+  float* tabs = (float*)((char*)seamR + r(gl_seam_floats(CB, T, hop) * 4));
   const bool one = gl_one_pass(hop);
+  if (one) {
+    hipLaunchKernelGGL(gl_tables_kernel, dim3(1), dim3(256), 0, st, hop, tabs, tabs + NFFT);
+    MST_CHECK_LAUNCH();
+  }
   const float beta = momentum / (1.f + momentum);
   auto synth = [&](const float2* c, const float2* p, const float* m, int nb, float* out) {
-    return one ? gl_synth_launch(c, p, m, beta, c != nullptr, nb, T, hop, seamL, seamR, out, st)
+    return one ? gl_synth_launch(c, p, m, beta, c != nullptr, nb, T, hop, seamL, seamR, tabs, out, st)
                : istft2_launch(c, p, m, beta, c != nullptr, nb, T, hop, frames, out, st);
   };
   {
