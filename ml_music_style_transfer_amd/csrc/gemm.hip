@@ -39,6 +39,53 @@ constexpr int MAXCLS = 8;              // wgrad K classes
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
 
+// fp32 products on the bf16 matrix cores ("bf16x6"): every fp32 operand is split exactly into
+// three bf16 pieces x = x0 + x1 + x2 (round-to-nearest at each step: the residual x - x0 has at
+// most 16 significant bits and x1 - r1 at most 8, so the split loses nothing for normal
+// values), and a . b = sum of the six products xi yj with i + j <= 2: the three dropped terms
+// are below 2^-24 relative, the size of the fp32 path's own rounding. Each bf16 x bf16
+// product is exact and v_mfma_f32_32x32x16_bf16 accumulates in fp32, so the result carries
+// fp32-level error (tests/test_gpu_kernels.py bounds it with the fp32 tolerances) at 6 MFMAs
+// of 32 cycles per 16-deep k step instead of 8 fp32 MFMAs of 64 cycles: 2.7x less matrix-
+// core time. MST_GEMM_X6=0 builds the fp32-MFMA inner loop instead.
+#ifndef MST_GEMM_X6
+#define MST_GEMM_X6 1
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+struct Split3 {
+  bf16x8 h, m, l;
+};
+
+// 8 consecutive fp32 (two 16-byte LDS reads) -> three bf16 planes
+__device__ __forceinline__ Split3 split3(const float* q) {
+  const f32x4 u = *reinterpret_cast<const f32x4*>(q);
+  const f32x4 w = *reinterpret_cast<const f32x4*>(q + 4);
+  Split3 s;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const float x = i < 4 ? u[i] : w[i - 4];
+    const __bf16 b0 = (__bf16)x;
+    const float r1 = x - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    const float r2 = r1 - (float)b1;
+    s.h[i] = b0;
+    s.m[i] = b1;
+    s.l[i] = (__bf16)r2;
+  }
+  return s;
+}
+
+// acc += a . b over one 16-deep k step, smallest products first
+__device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
+  return acc;
+}
+
 struct GP {
   int M, N, K, nk, splitk;
   long long nA, nP, nx0, nx1;  // elements addressable through each operand descriptor
@@ -377,6 +424,20 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
+#if MST_GEMM_X6
+    // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
+    const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 8;
+    const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 8;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const Split3 a0 = split3(As + 16 * s), a1 = split3(As + 32 * LDK + 16 * s);
+      const Split3 b0 = split3(Bs + 16 * s), b1 = split3(Bs + 32 * LDK + 16 * s);
+      acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+      acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+      acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+      acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+    }
+#else
     const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
     const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
 #pragma unroll
@@ -393,6 +454,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
       }
     }
+#endif
   };
 
   // Pipeline: LDS double buffer + two register stages. Iteration k issues the global loads of
@@ -425,10 +487,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
       // GEMM (A/B: conv fwd +5-10 %, dgrad +9-13 %, wgrad +15-25 %); left to the scheduler
       // they sink next to their wait.
       constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
+      constexpr int NMF = MST_GEMM_X6 ? 48 : 64;                 // MFMAs per tile per wave
+      constexpr int PER = NMF / NV > 2 ? 2 : (NMF / NV < 1 ? 1 : NMF / NV);
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x8, 2, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
       }
       store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
