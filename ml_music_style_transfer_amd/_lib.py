@@ -100,6 +100,7 @@ SIGNATURES = {
                                    c_size_t, c_void_p]),
     "mst_onoff_f32": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
     "mst_version": (ctypes.c_char_p, []),
+    "mst_gemm_products": (c_int32, []),
     "mst_device_arch": (c_int32, [ctypes.c_char_p, c_int32]),
 }
 

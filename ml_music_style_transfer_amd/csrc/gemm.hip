@@ -993,6 +993,8 @@ int wgrad_sources(const mst_wgrad_desc* d, mst_src* srcs, float** outs) {
 
 extern "C" {
 
+int mst_gemm_products(void) { return MST_GEMM_X6 ? 6 : 1; }
+
 size_t mst_conv_fwd_workspace_size(const mst_conv_desc* d) {
   GP p;
   if (build_conv(d, p) != MST_OK) return 0;
