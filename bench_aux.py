@@ -105,8 +105,34 @@ def _measured_traffic(kernel_key):
     return None, None
 
 
-def _roof(achieved_gbs, kernel, bytes_per_launch, traffic_key=None):
-    traffic, src = _measured_traffic(traffic_key) if traffic_key else (None, None)
+def _gl_traffic(n_iter):
+    """HBM bytes of one Griffin-Lim call from the newest round's PMC passes over the Griffin-Lim
+    leg (profiles/r*/gl_traffic.json): (n_iter + 1) syntheses (+ seam passes), n_iter complex
+    STFTs and the one magnitude transpose, each 2 x FETCH_SIZE + WRITE_SIZE per launch."""
+    pdir = os.path.join(ROOT, "profiles")
+    for r in sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) if os.path.isdir(pdir) else []:
+        tj = os.path.join(pdir, r, "gl_traffic.json")
+        if not os.path.exists(tj):
+            continue
+        d = json.load(open(tj))
+        per = {}
+        for k, v in d.get("per_kernel", {}).items():
+            for key in ("gl_synth_kernel", "gl_seam_kernel", "stft_kernel<3>", "transpose_mag_kernel"):
+                if key in k:
+                    per[key] = 2 * v["fetch_raw_per_launch"] + v["write_per_launch"]
+        if "gl_synth_kernel" not in per or "stft_kernel<3>" not in per:
+            continue
+        tot = ((n_iter + 1) * (per["gl_synth_kernel"] + per.get("gl_seam_kernel", 0.0))
+               + n_iter * per["stft_kernel<3>"] + per.get("transpose_mag_kernel", 0.0))
+        return round(tot), f"profiles/{r}/gl_traffic.json ({d.get('build', '')})"
+    return None, None
+
+
+def _roof(achieved_gbs, kernel, bytes_per_launch, traffic_key=None, traffic=None):
+    if traffic is not None:
+        traffic, src = traffic
+    else:
+        traffic, src = _measured_traffic(traffic_key) if traffic_key else (None, None)
     out = {"bound": "hbm", "kernel": kernel, "achieved": round(achieved_gbs, 1),
            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
            "traffic": traffic, "algorithmic_bytes_per_launch": int(bytes_per_launch)}
@@ -229,8 +255,9 @@ def griffinlim(args, world, rank, dev):
                   "clips/s", world, steps, 1, dt * 1e3,
                   {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
                    "L": L, "n_fft": 2048, "hop": bench.HOP},
-                  _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9, "istft_kernel + stft_kernel<COMPLEX> per iteration",
-                        B * n_iter * bpi), cpu, {"kernel_ms": round(kms, 3)})]
+                  _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
+                        "gl_synth_kernel + gl_seam_kernel + stft_kernel<COMPLEX> per iteration",
+                        B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, {"kernel_ms": round(kms, 3)})]
 
 
 def mss(args, world, rank, dev):

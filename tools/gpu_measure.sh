@@ -27,6 +27,11 @@ for what in "$@"; do
         python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcaux_write" -o run -- \
         python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_write.log" 2>&1 ;;
+    pmcgl)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcgl_fetch" -o run -- \
+        python3 bench_aux.py --workload griffinlim --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcgl_fetch.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcgl_write" -o run -- \
+        python3 bench_aux.py --workload griffinlim --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcgl_write.log" 2>&1 ;;
     aux)
       timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
     layers)
