@@ -16,12 +16,12 @@ for what in "$@"; do
       timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err" ;;
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-aux > "$OUT/prof_bench.json" 2> "$OUT/prof.err" ;;
     pmc)
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_fetch.log" 2>&1
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmc_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
-        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --kernel-timing-steps 0 > "$OUT/pmc_write.log" 2>&1 ;;
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmc_write.log" 2>&1 ;;
     pmcaux)
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcaux_fetch" -o run -- \
         python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_fetch.log" 2>&1
