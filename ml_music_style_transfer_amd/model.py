@@ -47,11 +47,19 @@ def slot_view(buf, p):
     return buf.view_as(p)
 
 
-# MST_WGRAD_STREAM=1 runs the weight-gradient GEMMs on a side stream (engine.GradSink). Off by
-# default: measured on one box it gained 0.6 % (49.92 -> 49.63 ms/step,
-# profiles/r02/bench_m7_wgrad_stream.txt) -- the GEMMs' losses are per-tile overheads more than
-# tail waves -- while the per-kernel roofline timing stops meaning anything once kernels overlap.
-_WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "0") == "1"
+# The weight-gradient GEMMs run on a side stream (engine.GradSink), concurrently with the
+# input-gradient GEMMs. With the fp32-MFMA GEMMs it gained 0.6 % (profiles/r02/
+# bench_m7_wgrad_stream.txt); with the shorter bf16x6 GEMMs 2.2 % (44.71 -> 43.84 ms/step,
+# profiles/r02/bench_m15_*.json), so it is on by default. MST_WGRAD_STREAM=0 turns it off;
+# set_wgrad_stream(False) does too (bench.py's per-launch timing leg: overlapping kernels
+# would make per-launch times meaningless). Stream capture (graphs.py) always runs serially.
+_WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "1") == "1"
+
+
+def set_wgrad_stream(on):
+    """Enable / disable the side stream for weight-gradient GEMMs (process-wide)."""
+    global _WGRAD_STREAM
+    _WGRAD_STREAM = bool(on)
 
 
 def _require_cuda(*ts):
@@ -403,7 +411,7 @@ class PerformanceNet(nn.Module):
             o, n = ent
             return slot_view(f["grad"][o:o + n], p)
         side = None
-        if _WGRAD_STREAM:  # weight-gradient GEMMs on a side stream (engine.GradSink)
+        if _WGRAD_STREAM and not torch.cuda.is_current_stream_capturing():
             dev = f["grad"].device if f is not None else torch.device("cuda", torch.cuda.current_device())
             side = self.__dict__.get("_mst_side")
             if side is None or side.device != dev:

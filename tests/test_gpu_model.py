@@ -249,6 +249,36 @@ def test_adam_inside_backward_matches_step(cuda):
     assert torch.equal(p0, p1) and torch.equal(m0, m1) and torch.equal(v0, v1)
 
 
+def test_wgrad_side_stream_bitwise(cuda):
+    """Weight-gradient GEMMs on the side stream (the default) produce bitwise the same
+    gradients as the serial order, at the training batch's time axis, with and without
+    backward Adam (which joins the side stream before each bucket update)."""
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd import model as M
+    from ml_music_style_transfer_amd.train import make_optimizer
+    xm, xa, cd, tg = _inputs(2, 252, cuda)
+    keep = M._WGRAD_STREAM
+    try:
+        for overlap in (False, True):
+            res = []
+            for side in (False, True):
+                M.set_wgrad_stream(side)
+                net = _det_model(cuda).eval()
+                opt = make_optimizer(net, lr=1e-3)
+                if overlap:
+                    opt.overlap_backward(bucket_bytes=8 << 20)
+                opt.zero_grad()
+                E.l1_loss(net(xm, xa, cd), tg).backward()
+                _, g, _ = net.flat_buffers()
+                g = g.clone()
+                opt.step()
+                res.append((g, net.flat_buffers()[0].clone()))
+            assert torch.equal(res[0][0], res[1][0]), overlap
+            assert torch.equal(res[0][1], res[1][1]), overlap
+    finally:
+        M.set_wgrad_stream(keep)
+
+
 def test_backward_gradient_order_matches_flat_layout(cuda):
     """The flat gradient buffer is laid out in engine.backward_param_order so that
     data-parallel buckets complete front to back; check the backward program really
