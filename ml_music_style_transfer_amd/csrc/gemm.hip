@@ -47,9 +47,10 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // product is exact and v_mfma_f32_32x32x16_bf16 accumulates in fp32, so the result carries
 // fp32-level error (tests/test_gpu_kernels.py bounds it with the fp32 tolerances) at 6 MFMAs
 // of 32 cycles per 16-deep k step instead of 8 fp32 MFMAs of 64 cycles: 2.7x less matrix-
-// core time. MST_GEMM_X6=0 builds the fp32-MFMA inner loop instead.
+// core time. MST_GEMM_X6=0 builds the fp32-MFMA inner loop instead; MST_GEMM_X6=1 keeps fp32
+// tiles in LDS and splits after every LDS read (each element split by both waves reading it).
 #ifndef MST_GEMM_X6
-#define MST_GEMM_X6 1
+#define MST_GEMM_X6 2  // 2: split once at the LDS store (default); 1: split after each LDS read
 #endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct Split3 {
@@ -74,6 +75,44 @@ __device__ __forceinline__ Split3 split3(const float* q) {
   }
   return s;
 }
+
+// MST_GEMM_X6 == 2 (default): the split happens once per element, when a loaded tile is stored:
+// A and B sit in LDS as three bf16 planes (hi, mid, lo) of [row][k] with 40-element rows (80 B:
+// the 16-byte fragment reads of 16 consecutive rows hit disjoint bank quads). The 6 planes
+// (60 KB) take ONE buffer (the 64 KB epilogue tile aliases it), so two workgroups still fit per
+// CU: the tile loop stores, syncs, runs the MFMAs, syncs, and the other workgroup on the CU
+// fills the store phase. Each element is split once instead of by both waves that read it.
+constexpr int LDKB = BK + 8;
+constexpr int PLANE = BM * LDKB;  // bf16 elements per plane (BM == BN)
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split_store4(__bf16* plane0, int off, const f32x4 v) {
+  bf16x4 hi, mid, lo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x = v[i];
+    const __bf16 b0 = (__bf16)x;
+    const float r1 = x - (float)b0;
+    const __bf16 b1 = (__bf16)r1;
+    hi[i] = b0;
+    mid[i] = b1;
+    lo[i] = (__bf16)(r1 - (float)b1);
+  }
+  *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
+  *reinterpret_cast<bf16x4*>(plane0 + PLANE + off) = mid;
+  *reinterpret_cast<bf16x4*>(plane0 + 2 * PLANE + off) = lo;
+}
+
+__device__ __forceinline__ Split3 ld_planes(const __bf16* q) {
+  Split3 s;
+  s.h = *reinterpret_cast<const bf16x8*>(q);
+  s.m = *reinterpret_cast<const bf16x8*>(q + PLANE);
+  s.l = *reinterpret_cast<const bf16x8*>(q + 2 * PLANE);
+  return s;
+}
+
+constexpr int LDS_NBUF = MST_GEMM_X6 == 2 ? 1 : 2;
+constexpr int LDS_FLOATS = MST_GEMM_X6 == 2 ? BM * BN : (BM + BN) * LDK;
 
 // acc += a . b over one 16-deep k step, smallest products first
 __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
@@ -238,7 +277,7 @@ __device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
 // One pass over K tiles [kt0, kt1) of output tile (m_t, n_t), then the epilogue: the final
 // values (direct), split-K slab `split`, or (slab != nullptr) a stream-K partial tile.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
-__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * LDK], int m_t,
+__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS], int m_t,
                                           int n_t, int kt0, int kt1, int split, float* slab) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -387,6 +426,26 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
 
   auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
     constexpr int st = decltype(S)::value;
+#if MST_GEMM_X6 == 2
+    (void)buf;
+    __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]);
+    __bf16* Bp = Ap + 3 * PLANE;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (AMODE == 2 && !WG)
+        split_store4(Ap, rm_row * LDKB + (kw + 2 * u) * 4, ra[st][u]);
+      else
+        split_store4(Ap, (km_row + 32 * u) * LDKB + km_kq, ra[st][u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (WG)
+        split_store4(Bp, (km_row + 32 * u) * LDKB + km_kq, rb[st][u]);
+      else
+        split_store4(Bp, rm_row * LDKB + (kw + 2 * u) * 4, rb[st][u]);
+    }
+    return;
+#endif
     float* As = lds[buf];
     float* Bs = lds[buf] + BM * LDK;
 #pragma unroll
@@ -424,7 +483,21 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-#if MST_GEMM_X6
+#if MST_GEMM_X6 == 2
+    // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
+    (void)buf;
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]) + (wm * 64 + r32) * LDKB + h * 8;
+    const __bf16* Bp = reinterpret_cast<const __bf16*>(lds[0]) + 3 * PLANE + (wn * 64 + r32) * LDKB + h * 8;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const Split3 a0 = ld_planes(Ap + 16 * s), a1 = ld_planes(Ap + 32 * LDKB + 16 * s);
+      const Split3 b0 = ld_planes(Bp + 16 * s), b1 = ld_planes(Bp + 32 * LDKB + 16 * s);
+      acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+      acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+      acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+      acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+    }
+#elif MST_GEMM_X6
     // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
     const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 8;
     const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 8;
@@ -494,6 +567,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
         __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
         __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
       }
+      if constexpr (MST_GEMM_X6 == 2) __syncthreads();  // one buffer: its MFMA reads first
       store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
     };
@@ -523,7 +597,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
 
   // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores ----
   __syncthreads();
-  float* Cs = &lds[0][0];  // 128 x 128 floats (64 KB) fits in the 72 KB of A/B buffers
+  float* Cs = &lds[0][0];  // 128 x 128 floats (64 KB): the A/B buffers' space
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -565,7 +639,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[(BM + BN) * 
 // the same work, so there is no partial last wave.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2][(BM + BN) * LDK];
+  static_assert(LDS_NBUF * LDS_FLOATS >= BM * BN, "epilogue tile must fit the A/B buffers");
+  static_assert(MST_GEMM_X6 != 2 || 3 * PLANE <= LDS_FLOATS, "bf16 planes must fit");
+  __shared__ __attribute__((aligned(16))) float lds[LDS_NBUF][LDS_FLOATS];
   const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
   if (p.sk_L == 0) {
     const int W = nx * ny * (int)gridDim.z;
