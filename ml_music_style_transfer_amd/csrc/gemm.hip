@@ -173,10 +173,6 @@ struct GP {
   long long ldo, ldc, ldt;  // column of (c, tap) = c * ldc + tap * ldt
   int taps, ocustom;
   float inv_taps;
-  // wgrad N order: n = c * taps + tap (ntap = 0), or n = tap * nC + c (ntap = 1) when the output
-  // is tap-major (ldt > ldc): consecutive n are then consecutive addresses in the epilogue
-  int ntap, nC;
-  float inv_nC;
   float scale;
   int accumulate;
   // split-K slab
@@ -239,10 +235,7 @@ __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
 __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) {
   if (m >= p.M || n >= p.N) return;
   long long col = n;  // n = c * taps + tap: the column in the torch layout
-  if (p.ntap) {       // n = tap * nC + c: tap-major weights, column = c * ldc + tap * ldt
-    const int tap = (int)(((float)n + 0.5f) * p.inv_nC);  // exact for n < 2^22
-    col = (long long)(n - tap * p.nC) * p.ldc + (long long)tap * p.ldt;
-  } else if (p.ocustom) {  // other layouts: column = c * ldc + tap * ldt
+  if (p.ocustom) {    // e.g. tap-major weights: column = c * ldc + tap * ldt
     const int c = (int)(((float)n + 0.5f) * p.inv_taps);  // exact for n < 2^22
     col = (long long)c * p.ldc + (long long)(n - c * p.taps) * p.ldt;
   }
@@ -351,9 +344,8 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     for (int u = 0; u < 4; ++u) {
       const int m = m0 + km_row + 32 * u;
       const int n = n0 + km_row + 32 * u;
-      // N order: n = c * taps + tap, or tap * nC + c for a tap-major output (p.ntap)
-      const int tap = p.ntap ? n / p.nC : n - (n / TAPS) * TAPS;
-      const int c = p.ntap ? n - tap * p.nC : n / TAPS;
+      const int c = n / TAPS;  // N order n = c * taps + tap for every output layout
+      const int tap = n - c * TAPS;
       const int abase = m * p.sPc + bdl * (int)p.sPb + t0ref + tlb;
       const int tin0 = p.ta * (t0ref + tlb) + p.tb + p.tg * tap;  // input time at i = 0
       const int bbase = c * p.sc0 + bdl * (int)p.sb0 + tin0 + p.off0;
@@ -1055,12 +1047,6 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   }
   p.ocustom = !(p.ldc == d->taps && p.ldt == 1);
   p.inv_taps = 1.0f / (float)d->taps;
-  // tap-major outputs (the model's weight slots: ldc = 1, ldt = Cin) take the tap-major N order,
-  // so the epilogue's row-contiguous stores land on contiguous addresses (with the c-major order
-  // consecutive n were ldt apart: 4-byte scattered stores, 3-4x slower weight gradients)
-  p.ntap = d->taps > 1 && p.ldt > p.ldc ? 1 : 0;
-  p.nC = src.C;
-  p.inv_nC = 1.0f / (float)src.C;
   MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
