@@ -82,33 +82,74 @@ __device__ __forceinline__ Split3 split3(const float* q) {
 // (60 KB) take ONE buffer (the 64 KB epilogue tile aliases it), so two workgroups still fit per
 // CU: the tile loop stores, syncs, runs the MFMAs, syncs, and the other workgroup on the CU
 // fills the store phase. Each element is split once instead of by both waves that read it.
-constexpr int LDKB = BK + 8;
+// Plane rows are 64 B (32 bf16, no padding) with the four 16-byte quads of row r XOR-swizzled by
+// (r >> 2) & 3: a 16-row fragment read (16-byte lanes) and a 4-row k-major write (8-byte lanes,
+// 8 per row) each cover every bank once, and the row-major writes pair two k quads into one
+// 16-byte store per plane (their unit order, rm_quad, makes a thread's quads adjacent).
+constexpr int LDKB = BK;
 constexpr int PLANE = BM * LDKB;  // bf16 elements per plane (BM == BN)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ void split_store4(__bf16* plane0, int off, const f32x4 v) {
+__device__ __forceinline__ int pl_off(int row, int q) {  // element offset of (row, 16-B quad q)
+  return row * LDKB + 8 * (q ^ ((row >> 2) & 3));
+}
+
+struct Bf3 {
+  __bf16 h, m, l;
+};
+__device__ __forceinline__ Bf3 split1(float x) {
+  const __bf16 b0 = (__bf16)x;
+  const float r1 = x - (float)b0;
+  const __bf16 b1 = (__bf16)r1;
+  return Bf3{b0, b1, (__bf16)(r1 - (float)b1)};
+}
+
+// 4 consecutive k (k0 = 4 c8) of one row: three 8-byte stores
+__device__ __forceinline__ void split_store4(__bf16* plane0, int row, int c8, const f32x4 v) {
   bf16x4 hi, mid, lo;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const float x = v[i];
-    const __bf16 b0 = (__bf16)x;
-    const float r1 = x - (float)b0;
-    const __bf16 b1 = (__bf16)r1;
-    hi[i] = b0;
-    mid[i] = b1;
-    lo[i] = (__bf16)(r1 - (float)b1);
+    const Bf3 t = split1(v[i]);
+    hi[i] = t.h;
+    mid[i] = t.m;
+    lo[i] = t.l;
   }
+  const int off = pl_off(row, c8 >> 1) + 4 * (c8 & 1);
   *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
   *reinterpret_cast<bf16x4*>(plane0 + PLANE + off) = mid;
   *reinterpret_cast<bf16x4*>(plane0 + 2 * PLANE + off) = lo;
 }
 
-__device__ __forceinline__ Split3 ld_planes(const __bf16* q) {
+// 8 consecutive k (quad q) of one row from two units: three 16-byte stores
+__device__ __forceinline__ void split_store8(__bf16* plane0, int row, int q, const f32x4 v0,
+                                             const f32x4 v1) {
+  bf16x8 hi, mid, lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const Bf3 t = split1(i < 4 ? v0[i] : v1[i - 4]);
+    hi[i] = t.h;
+    mid[i] = t.m;
+    lo[i] = t.l;
+  }
+  const int off = pl_off(row, q);
+  *reinterpret_cast<bf16x8*>(plane0 + off) = hi;
+  *reinterpret_cast<bf16x8*>(plane0 + PLANE + off) = mid;
+  *reinterpret_cast<bf16x8*>(plane0 + 2 * PLANE + off) = lo;
+}
+
+__device__ __forceinline__ Split3 ld_planes(const __bf16* base, int row, int q) {
+  const __bf16* p = base + pl_off(row, q);
   Split3 s;
-  s.h = *reinterpret_cast<const bf16x8*>(q);
-  s.m = *reinterpret_cast<const bf16x8*>(q + PLANE);
-  s.l = *reinterpret_cast<const bf16x8*>(q + 2 * PLANE);
+  s.h = *reinterpret_cast<const bf16x8*>(p);
+  s.m = *reinterpret_cast<const bf16x8*>(p + PLANE);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PLANE);
   return s;
+}
+
+// Row-major tile units: thread (row, kw) holds k quads rm_quad(kw, u), u = 0..3. The bf16-plane
+// path takes 4 kw + u (a thread's quads adjacent, stored in pairs); the fp32 path kw + 2 u.
+__device__ __forceinline__ constexpr int rm_quad(int kw, int u) {
+  return MST_GEMM_X6 == 2 ? 4 * kw + u : kw + 2 * u;
 }
 
 constexpr int LDS_NBUF = MST_GEMM_X6 == 2 ? 1 : 2;
@@ -288,9 +329,10 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
 
   // Two unit mappings of a 128-row x 32-k tile onto 256 threads, 4 units of 4 consecutive k:
   //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7 -> 8 lanes run along k
-  //   RM ("row-major"): row = tid&127, k quads kw + 2u    -> lanes run along rows; k is
+  //   RM ("row-major"): row = tid&127, k quads rm_quad(kw, u) -> lanes run along rows; k is
   //                     wave-uniform (kw = tid>>7 via readfirstlane), so its decode is scalar
-  // Both store a unit as one conflict-free ds_write_b128 into the [row][k] LDS image.
+  // fp32 path: both store a unit as one conflict-free ds_write_b128 into the [row][k] image;
+  // bf16-plane path: see pl_off.
   // A: AMODE 1 (k-contiguous, float4) and 0 (k-scalar) use KM; AMODE 2 (m-contiguous) RM.
   // B: conv/dgrad (n = time, contiguous) RM; wgrad (k = time) KM.
   const int km_row = tid >> 3;
@@ -391,7 +433,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            ra[st_][u][i] = ldbs(rA, rowA[0], sA + (4 * (kw + 2 * u) + i) * p.sAc * 4);
+            ra[st_][u][i] = ldbs(rA, rowA[0], sA + (4 * rm_quad(kw, u) + i) * p.sAc * 4);
       }
       // ---------------- B: X(b, c, a*t + beta + g*tap), column per lane ----------------
       const int tin = tinb + p.tg * tap;
@@ -406,7 +448,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int c = cb + 4 * (kw + 2 * u) + i;  // wave-uniform
+          const int c = cb + 4 * rm_quad(kw, u) + i;  // wave-uniform
           rb[st_][u][i] = ldbs(mk_rsrc(xs, c < Cs ? ns : 0), lo, c * scb);
         }
     } else {
@@ -430,19 +472,19 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     (void)buf;
     __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]);
     __bf16* Bp = Ap + 3 * PLANE;
+    if constexpr (AMODE == 2 && !WG) {  // quads 4 kw + u: pairs (0, 1), (2, 3) are adjacent
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if constexpr (AMODE == 2 && !WG)
-        split_store4(Ap, rm_row * LDKB + (kw + 2 * u) * 4, ra[st][u]);
-      else
-        split_store4(Ap, (km_row + 32 * u) * LDKB + km_kq, ra[st][u]);
+      for (int u = 0; u < 4; u += 2) split_store8(Ap, rm_row, 2 * kw + u / 2, ra[st][u], ra[st][u + 1]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) split_store4(Ap, km_row + 32 * u, km_kq / 4, ra[st][u]);
     }
+    if constexpr (WG) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if constexpr (WG)
-        split_store4(Bp, (km_row + 32 * u) * LDKB + km_kq, rb[st][u]);
-      else
-        split_store4(Bp, rm_row * LDKB + (kw + 2 * u) * 4, rb[st][u]);
+      for (int u = 0; u < 4; ++u) split_store4(Bp, km_row + 32 * u, km_kq / 4, rb[st][u]);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; u += 2) split_store8(Bp, rm_row, 2 * kw + u / 2, rb[st][u], rb[st][u + 1]);
     }
     return;
 #endif
@@ -452,7 +494,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     for (int u = 0; u < 4; ++u) {
       const f32x4 v = ra[st][u];
       if constexpr (AMODE == 2 && !WG)
-        *reinterpret_cast<f32x4*>(As + rm_row * LDK + (kw + 2 * u) * 4) = v;
+        *reinterpret_cast<f32x4*>(As + rm_row * LDK + rm_quad(kw, u) * 4) = v;
       else
         *reinterpret_cast<f32x4*>(As + (km_row + 32 * u) * LDK + km_kq) = v;
     }
@@ -462,7 +504,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       if constexpr (WG)
         *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
       else
-        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + (kw + 2 * u) * 4) = v;
+        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + rm_quad(kw, u) * 4) = v;
     }
   };
 
@@ -486,12 +528,13 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
 #if MST_GEMM_X6 == 2
     // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
     (void)buf;
-    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]) + (wm * 64 + r32) * LDKB + h * 8;
-    const __bf16* Bp = reinterpret_cast<const __bf16*>(lds[0]) + 3 * PLANE + (wn * 64 + r32) * LDKB + h * 8;
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]);
+    const __bf16* Bp = Ap + 3 * PLANE;
+    const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      const Split3 a0 = ld_planes(Ap + 16 * s), a1 = ld_planes(Ap + 32 * LDKB + 16 * s);
-      const Split3 b0 = ld_planes(Bp + 16 * s), b1 = ld_planes(Bp + 32 * LDKB + 16 * s);
+      const Split3 a0 = ld_planes(Ap, ra0, 2 * s + h), a1 = ld_planes(Ap, ra0 + 32, 2 * s + h);
+      const Split3 b0 = ld_planes(Bp, rb0, 2 * s + h), b1 = ld_planes(Bp, rb0 + 32, 2 * s + h);
       acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
       acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
       acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
