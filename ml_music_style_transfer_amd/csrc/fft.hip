@@ -1306,13 +1306,18 @@ __global__ __launch_bounds__(256) void ola_kernel(const float* __restrict__ fram
 // Reads each bin once (20 B: cur, prev, mag), writes each sample once.
 // ---------------------------------------------------------------------------
 constexpr int GLW = 8;                      // waves per synthesis workgroup
-constexpr int GL_OWN = 16;                  // samples per thread
+constexpr int GL_OWN = 12;                  // samples per thread (G = 16 frames at hop 256)
 constexpr int GL_SEG = 64 * GLW * GL_OWN;   // samples a workgroup covers (8192)
 
 // frames per workgroup: the covered span (G - 1) hop + NFFT fits GL_SEG; whole rounds when G >= 8
 static inline int gl_frames(int hop) {
   const int g = (GL_SEG - NFFT) / hop + 1;
-  return g >= GLW ? g / GLW * GLW : g;
+  static const int cap = [] {  // MST_GL_FRAMES: a smaller G (A/B tuning)
+    const char* e = getenv("MST_GL_FRAMES");
+    return e ? atoi(e) : 0;
+  }();
+  const int gg = cap > 0 && cap < g ? cap : g;
+  return gg >= GLW ? gg / GLW * GLW : gg;
 }
 
 // Squared periodic Hann, sin^4(pi n / 2048) (the sin^2 form of the synthesis window), into an
