@@ -17,13 +17,18 @@
 // (+ one radix-2 stage for odd log2 n) over LDS, 2048 complex per chunk of frames.
 // Deterministic: fixed summation order everywhere; per-size launches accumulate into dpred
 // in stream order, reflect-pad edges are folded in by a final kernel.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 constexpr int RWIN = 4096;   // padded samples owned per workgroup
 constexpr int CAP = 2048;    // complex values per LDS FFT buffer
-constexpr int NT = 256;
+#ifndef MSS_NT
+#define MSS_NT 256
+#endif
+constexpr int NT = MSS_NT;  // threads per workgroup
 
 struct c2 {
   float x, y;
@@ -280,6 +285,268 @@ __global__ __launch_bounds__(NT) void mss_scale_kernel(const MssArgs a) {
   }
 }
 
+// Wave-local variant (the default): the same ownership (RWIN padded samples per workgroup, 3
+// halo frames) and the same arithmetic, but every transform runs inside one wave, in place in
+// that wave's LDS buffer (a radix-4 stage reads all its inputs into registers, then writes), so
+// no workgroup barrier sits inside an FFT. Per round each wave takes 2 FB consecutive frames:
+// pass A transforms the FB even ones and keeps their gradient spectra in registers, pass B the
+// FB odd ones; the pair-packed Hermitian spectra C = H^a + i H^b then go through one inverse
+// transform per pair. After a workgroup barrier every thread adds the round's frames covering
+// its RWIN / 256 owned samples (kept in registers) in increasing frame order, so the summation
+// order per sample is the frame order, as in the cooperative kernel above.
+template <bool INV>
+__device__ __forceinline__ c2 twq(const c2* qt, int m, int N) {  // W_N^m from the quarter table
+  m &= N - 1;
+  const int Q = N >> 2, q = m / Q, r = m & (Q - 1);
+  const c2 w = qt[r];
+  c2 o;
+  if (q == 0) o = w;
+  else if (q == 1) o = mk(w.y, -w.x);
+  else if (q == 2) o = mk(-w.x, -w.y);
+  else o = mk(-w.y, w.x);
+  if (INV) o.y = -o.y;
+  return o;
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// FB = BW / N transforms of size N = 2^LOG2N, in place in s[0 .. BW) (Stockham order per stage:
+// inputs read to registers, then outputs written), natural-order result.
+template <int LOG2N, int BW, bool INV>
+__device__ __forceinline__ void wave_fft(c2* s, const c2* qt, int lane) {
+  constexpr int N = 1 << LOG2N, NR = N / 4, IT = BW / 4 / 64;
+  int Ns = 1;
+#pragma unroll
+  for (int st = 0; st < LOG2N / 2; ++st) {
+    c2 v[IT][4];
+    int ln = lane;
+    __asm__ volatile("" : "+v"(ln));  // lane-derived addresses formed per stage, not kept live
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = ln + 64 * it, fr = idx / NR, j = idx - fr * NR;
+      const c2* src = s + fr * N + j;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[it][r] = src[r * NR];
+    }
+    wave_sync();
+    const int step = N / (Ns * 4);
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = ln + 64 * it, fr = idx / NR, j = idx - fr * NR;
+      const int k = j & (Ns - 1);
+      if (st > 0) {  // k step < N / 4: one quarter-table entry, its square and cube
+        c2 w1 = qt[k * step];
+        if (INV) w1.y = -w1.y;
+        const c2 w2 = cmul(w1, w1);
+        v[it][1] = cmul(v[it][1], w1);
+        v[it][2] = cmul(v[it][2], w2);
+        v[it][3] = cmul(v[it][3], cmul(w2, w1));
+      }
+      dft4<INV>(v[it][0], v[it][1], v[it][2], v[it][3]);
+      c2* d = s + fr * N + (j - k) * 4 + k;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) d[r * Ns] = v[it][r];
+    }
+    wave_sync();
+    Ns *= 4;
+  }
+  if constexpr (LOG2N & 1) {
+    constexpr int NR2 = N / 2, IT2 = BW / 2 / 64;
+    c2 v[IT2][2];
+    int ln = lane;
+    __asm__ volatile("" : "+v"(ln));
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int idx = ln + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
+      v[it][0] = s[fr * N + j];
+      v[it][1] = s[fr * N + j + NR2];
+    }
+    wave_sync();
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int idx = ln + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
+      const int k = j & (Ns - 1);
+      const c2 b = cmul(v[it][1], twq<INV>(qt, k, 2 * Ns));
+      c2* d = s + fr * N + (j - k) * 2 + k;
+      d[0] = v[it][0] + b;
+      d[Ns] = v[it][0] - b;
+    }
+    wave_sync();
+  }
+}
+
+template <int LOG2N>
+__global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(const MssArgs a) {
+  constexpr int N = 1 << LOG2N, H = N / 4, HALF = N / 2, NBIN = HALF + 1;
+  constexpr int W = 4;                       // waves per workgroup
+  constexpr int BW = N > 1024 ? N : 1024;    // complex per wave buffer
+  constexpr int FB = BW / N;                 // transforms per pass
+  constexpr int GF = 2 * FB;                 // frames per wave per round
+  constexpr int RF = W * GF;                 // frames per round
+  constexpr int NE = (FB * NBIN + 63) / 64;  // spectrum entries per lane
+  constexpr int OWN = RWIN / 256;            // owned samples per thread
+  __shared__ __attribute__((aligned(16))) c2 buf[W * BW];
+  __shared__ c2 qt[N / 4];
+  __shared__ float hw[N];
+  __shared__ float red[2][W];
+
+  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = (int)a.L;
+  const float* p = a.pred + (long long)b * a.L;
+  const float* q = a.target + (long long)b * a.L;
+  const bool grad = a.dpred != nullptr;
+  for (int r = tid; r < N / 4; r += 256) {
+    double sn, cs;
+    sincospi(2.0 * r / N, &sn, &cs);
+    qt[r] = mk((float)cs, (float)-sn);
+  }
+  for (int j = tid; j < N; j += 256) {
+    double sn, cs;
+    sincospi(2.0 * j / N, &sn, &cs);
+    hw[j] = (float)(0.5 - 0.5 * cs);  // periodic Hann
+  }
+  __syncthreads();
+
+  const int own_lo = w * RWIN;
+  const int f_own0 = w * (RWIN / H), f_own1 = min(f_own0 + RWIN / H, a.T);
+  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
+  c2* S = buf + wave * BW;
+  float acc[OWN];
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
+  float s_abs = 0.f, s_log = 0.f;
+
+#pragma unroll 1
+  for (int t_round = f_lo; t_round < f_own1; t_round += RF) {
+    const int t_base = t_round + wave * GF;  // this wave's first frame
+    if (t_base < f_own1) {                   // wave-uniform
+      c2 zga[NE], zgb[NE];
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        // load + window FB frames t_base + 2m + pass: z = w (p + i q)
+#pragma unroll 4
+        for (int k = 0; k < BW / 64; ++k) {
+          const int e = lane + 64 * k, m = e / N, j = e - m * N;
+          const int t = t_base + 2 * m + pass;
+          c2 z = mk(0.f, 0.f);
+          if (t < f_own1) {
+            const int src = reflect(t * H + j - HALF, L);
+            z = mk(hw[j] * p[src], hw[j] * q[src]);
+          }
+          S[e] = z;
+        }
+        wave_sync();
+        wave_fft<LOG2N, BW, false>(S, qt, lane);
+        // spectra, loss, gradient spectra (registers)
+#pragma unroll
+        for (int jj = 0; jj < NE; ++jj) {
+          int ln = lane;
+          __asm__ volatile("" : "+v"(ln));  // per-entry indices, not kept live across the loop
+          const int e = ln + 64 * jj, m = e / NBIN, f = e - m * NBIN;
+          const int t = t_base + 2 * m + pass;
+          c2 zg = mk(0.f, 0.f);
+          if (e < FB * NBIN && t < f_own1) {
+            const c2 zf = S[m * N + f], zr = S[m * N + ((N - f) & (N - 1))];
+            const c2 P = (zf + conjc(zr)) * 0.5f;
+            const c2 D = zf - conjc(zr);
+            const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
+            const float sp = sqrtf(P.x * P.x + P.y * P.y), st = sqrtf(Q.x * Q.x + Q.y * Q.y);
+            const float lp = logf(sp + a.eps), lt = logf(st + a.eps);
+            if (t >= f_own0) {
+              s_abs += fabsf(sp - st);
+              s_log += fabsf(lp - lt);
+            }
+            if (grad && sp > 0.f) {
+              const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
+              const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
+              zg = P * (g / sp);
+            }
+          }
+          if (pass == 0) zga[jj] = zg;
+          else zgb[jj] = zg;
+        }
+        wave_sync();  // every lane has read the spectra before S is overwritten
+      }
+      if (grad) {
+        // C = H^a + i H^b per pair (H^a_f = Za/2, H^a_{n-f} = conj(Za)/2)
+#pragma unroll
+        for (int jj = 0; jj < NE; ++jj) {
+          int ln = lane;
+          __asm__ volatile("" : "+v"(ln));
+          const int e = ln + 64 * jj, m = e / NBIN, f = e - m * NBIN;
+          if (e < FB * NBIN) {
+            const c2 za = zga[jj], zb = zgb[jj];
+            c2* c = S + m * N;
+            if (f == 0 || f == HALF) {
+              c[f] = mk(za.x, zb.x);
+            } else {
+              c[f] = mk(0.5f * (za.x - zb.y), 0.5f * (za.y + zb.x));
+              c[N - f] = mk(0.5f * (za.x + zb.y), 0.5f * (-za.y + zb.x));
+            }
+          }
+        }
+        wave_sync();
+        wave_fft<LOG2N, BW, true>(S, qt, lane);
+      }
+    }
+    if (!grad) continue;  // uniform over the workgroup: no barrier needed
+    __syncthreads();      // every wave's gradient frames are in its buffer
+    // windowed overlap-add of the round's frames into the owned samples, frames in order
+    const int r_hi = min(t_round + RF, f_own1);
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const int sp = own_lo + tid + 256 * i;  // padded coordinate
+      const int th = sp / H;
+      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
+      float v = acc[i];
+      for (int t = t0; t <= t1; ++t) {
+        const int j = sp - t * H;
+        const int rel = t - t_round, ww = rel / GF, m = (rel - ww * GF) >> 1;
+        const c2 g = buf[ww * BW + m * N + j];
+        v += hw[j] * ((rel & 1) ? g.y : g.x);
+      }
+      acc[i] = v;
+    }
+    __syncthreads();  // the buffers are read before the next round overwrites them
+  }
+
+  s_abs = wave_sum(s_abs);
+  s_log = wave_sum(s_log);
+  if (lane == 0) {
+    red[0][wave] = s_abs;
+    red[1][wave] = s_log;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float sa = 0.f, sl = 0.f;
+    for (int i = 0; i < W; ++i) {
+      sa += red[0][i];
+      sl += red[1][i];
+    }
+    a.partial[((long long)b * a.nwg + w) * 2] = sa;
+    a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
+  }
+  if (!grad) return;
+  float* dp = a.dpred + (long long)b * a.L;
+  float* ed = a.edges + (long long)b * N;
+  const int own_hi = min(own_lo + RWIN, L + N);
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const int pp = own_lo + tid + 256 * i;
+    if (pp >= own_hi) continue;
+    const float v = acc[i];
+    const int x = pp - HALF;
+    if (x < 0) ed[pp] = v;
+    else if (x >= L) ed[HALF + (x - L)] = v;
+    else dp[x] = a.accumulate ? dp[x] + v : v;
+  }
+}
+
 // dpred += reflect-pad edge gradients of every size (in size order: deterministic).
 struct FoldArgs {
   float* dpred;
@@ -338,6 +605,15 @@ __global__ void mss_loss_kernel(const LossArgs a) {
     for (int i = 0; i < (int)(blockDim.x / 64); ++i) t += red[i];
     a.loss[0] = (float)t;
   }
+}
+
+// MST_MSS_LEGACY=1: the workgroup-cooperative kernel (A/B)
+bool mss_legacy() {
+  static const bool v = [] {
+    const char* e = getenv("MST_MSS_LEGACY");
+    return e && atoi(e) != 0;
+  }();
+  return v;
 }
 
 int log2i(int n) {
@@ -408,13 +684,24 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     a.edges = w + pl.edge_off[s];
     a.partial = w + pl.part_off[s];
     dim3 grid(pl.nwg[s], (unsigned)B);
-    switch (log2i(pl.n[s])) {
-      case 6: mss_scale_kernel<6><<<grid, NT, 0, st>>>(a); break;
-      case 7: mss_scale_kernel<7><<<grid, NT, 0, st>>>(a); break;
-      case 8: mss_scale_kernel<8><<<grid, NT, 0, st>>>(a); break;
-      case 9: mss_scale_kernel<9><<<grid, NT, 0, st>>>(a); break;
-      case 10: mss_scale_kernel<10><<<grid, NT, 0, st>>>(a); break;
-      default: mss_scale_kernel<11><<<grid, NT, 0, st>>>(a); break;
+    if (mss_legacy()) {
+      switch (log2i(pl.n[s])) {
+        case 6: mss_scale_kernel<6><<<grid, NT, 0, st>>>(a); break;
+        case 7: mss_scale_kernel<7><<<grid, NT, 0, st>>>(a); break;
+        case 8: mss_scale_kernel<8><<<grid, NT, 0, st>>>(a); break;
+        case 9: mss_scale_kernel<9><<<grid, NT, 0, st>>>(a); break;
+        case 10: mss_scale_kernel<10><<<grid, NT, 0, st>>>(a); break;
+        default: mss_scale_kernel<11><<<grid, NT, 0, st>>>(a); break;
+      }
+    } else {
+      switch (log2i(pl.n[s])) {
+        case 6: mss_wave_kernel<6><<<grid, 256, 0, st>>>(a); break;
+        case 7: mss_wave_kernel<7><<<grid, 256, 0, st>>>(a); break;
+        case 8: mss_wave_kernel<8><<<grid, 256, 0, st>>>(a); break;
+        case 9: mss_wave_kernel<9><<<grid, 256, 0, st>>>(a); break;
+        case 10: mss_wave_kernel<10><<<grid, 256, 0, st>>>(a); break;
+        default: mss_wave_kernel<11><<<grid, 256, 0, st>>>(a); break;
+      }
     }
     MST_CHECK_LAUNCH();
   }

@@ -36,6 +36,24 @@ for what in "$@"; do
       timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
     layers)
       timeout -k 10 300 python -u tools/gemm_layers.py > "$OUT/gemm_layers.txt" 2> "$OUT/gemm_layers.err" ;;
+    msstest)
+      timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -k "multiscale or mss" > "$OUT/pytest_mss.log" 2>&1 ;;
+    abmss)
+      MST_MSS_LEGACY=1 timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_legacy.json" 2>&1
+      timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_wave.json" 2>&1
+      MST_LIB_PATH=ml_music_style_transfer_amd/csrc/build_nt512/libmst_hip.so MST_MSS_LEGACY=1 \
+        timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_legacy_nt512.json" 2>&1 ;;
+    gltest)
+      timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -k "griffinlim or istft" > "$OUT/pytest_gl.log" 2>&1 ;;
+    auxgl)
+      timeout -k 10 300 python -u bench_aux.py --workload griffinlim --no-cpu-baseline > "$OUT/aux_gl.json" 2> "$OUT/aux_gl.err" ;;
+    auxmss)
+      timeout -k 10 300 python -u bench_aux.py --workload mss --no-cpu-baseline > "$OUT/aux_mss.json" 2> "$OUT/aux_mss.err" ;;
+    profaux)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profaux" -o run -- \
+        python3 bench_aux.py --no-cpu-baseline --steps 5 --warmup 2 > "$OUT/profaux.json" 2> "$OUT/profaux.err" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
