@@ -107,7 +107,7 @@ def _measured_traffic(kernel_key):
 
 def _gl_traffic(n_iter):
     """HBM bytes of one Griffin-Lim call from the newest round's PMC passes over the Griffin-Lim
-    leg (profiles/r*/gl_traffic.json): (n_iter + 1) syntheses (+ seam passes), n_iter complex
+    leg (profiles/r*/gl_traffic.json): (n_iter + 1) syntheses (+ seam passes before round 3), n_iter complex
     STFTs and the one magnitude transpose, each 2 x FETCH_SIZE + WRITE_SIZE per launch."""
     pdir = os.path.join(ROOT, "profiles")
     for r in sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) if os.path.isdir(pdir) else []:
@@ -256,7 +256,7 @@ def griffinlim(args, world, rank, dev):
                   {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
                    "L": L, "n_fft": 2048, "hop": bench.HOP},
                   _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
-                        "gl_synth_kernel + gl_seam_kernel + stft_kernel<COMPLEX> per iteration",
+                        "gl_synth_kernel (atomic seams) + stft_kernel<COMPLEX> per iteration",
                         B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, {"kernel_ms": round(kms, 3)})]
 
 

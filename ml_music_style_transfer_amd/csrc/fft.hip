@@ -1316,8 +1316,11 @@ static inline int gl_frames(int hop) {
     const char* e = getenv("MST_GL_FRAMES");
     return e ? atoi(e) : 0;
   }();
-  const int gg = cap > 0 && cap < g ? cap : g;
-  return gg >= GLW ? gg / GLW * GLW : gg;
+  int gg = cap > 0 && cap < g ? cap : g;
+  gg = gg >= GLW ? gg / GLW * GLW : gg;
+  // G hop >= NFFT - hop: no sample is covered by more than two workgroups, so a seam is the sum
+  // of exactly two atomic adds (order-independent)
+  return max(gg, ceil_div(NFFT - hop, hop));
 }
 
 // Squared periodic Hann, sin^4(pi n / 2048) (the sin^2 form of the synthesis window), into an
@@ -1390,8 +1393,7 @@ __global__ __launch_bounds__(512, 4) void gl_synth_kernel(const float2* __restri
                                                           float beta, int normalize, int T,
                                                           int hop, int G, int nwg,
                                                           float* __restrict__ y,
-                                                          float* __restrict__ seamL,
-                                                          float* __restrict__ seamR) {
+                                                          float* __restrict__ ynext) {
   __shared__ __attribute__((aligned(16))) c2 scratch[GLW * SCR];
   __shared__ float h2[NFFT];
   const int b = blockIdx.y, wg = blockIdx.x;
@@ -1493,72 +1495,26 @@ __global__ __launch_bounds__(512, 4) void gl_synth_kernel(const float2* __restri
   }
   const int cov_end = (F1 - 1) * hop + NFFT;
   float* yr = y + (long long)b * L;
-  const long long seam0 = (long long)b * (nwg - 1);
+  float* yn = ynext ? ynext + (long long)b * L : nullptr;
 #pragma unroll
   for (int i = 0; i < GL_OWN; ++i) {
     const int sp = c0 + threadIdx.x + 512 * i;
     if (sp >= cov_end) continue;
-    const int fmin = (sp - NFFT) >= 0 ? div_hop(sp - NFFT, hop, inv_hop) + 1 : 0;
-    const int fmax = min(div_hop(sp, hop, inv_hop), T - 1);
-    if (F0 > 0 && fmin < F0) {  // shared with the previous workgroup (its right seam)
-      seamL[(seam0 + wg - 1) * NFFT + (sp - c0)] = acc[i];
-      continue;
-    }
-    if (F1 < T && fmax >= F1) {  // shared with the next workgroup
-      seamR[(seam0 + wg) * NFFT + (sp - F1 * hop)] = acc[i];
-      continue;
-    }
     const int s = sp - NFFT / 2;
     if (s < 0 || s >= L) continue;
+    const int fmin = (sp - NFFT) >= 0 ? div_hop(sp - NFFT, hop, inv_hop) + 1 : 0;
+    const int fmax = min(div_hop(sp, hop, inv_hop), T - 1);
     const float wss = gl_wss(h2, sp, fmin, fmax, hop);
-    yr[s] = wss > 1.17549435e-38f ? acc[i] * __builtin_amdgcn_rcpf(wss) : acc[i];
-  }
-}
-
-// Hann^2 (2048) and, when hop divides NFFT, the interior window-sum-square by sample phase
-// (hop entries, frames summed in increasing order): built once per Griffin-Lim call.
-__global__ __launch_bounds__(256) void gl_tables_kernel(int hop, float* __restrict__ h2g,
-                                                        float* __restrict__ wssr) {
-  __shared__ float h2[NFFT];
-  gl_fill_h2(h2);
-  __syncthreads();
-  for (int n = threadIdx.x; n < NFFT; n += blockDim.x) h2g[n] = h2[n];
-  if (NFFT % hop == 0)
-    for (int r = threadIdx.x; r < hop; r += blockDim.x) {
-      float s = 0.f;
-      for (int k = NFFT / hop - 1; k >= 0; --k) s += h2[r + hop * k];
-      wssr[r] = s;
-    }
-}
-
-// The NFFT - hop samples of seam j of clip b (between synthesis workgroups j and j + 1): right
-// partial (frames of workgroup j) + left partial, then / wss.
-__global__ __launch_bounds__(256) void gl_seam_kernel(const float* __restrict__ seamL,
-                                                      const float* __restrict__ seamR, int T,
-                                                      int hop, int G, int nwg,
-                                                      const float* __restrict__ h2g,
-                                                      const float* __restrict__ wssr,
-                                                      float* __restrict__ y) {
-  const int b = blockIdx.y, j = blockIdx.x;
-  const int L = hop * (T - 1);
-  const int base = (j + 1) * G * hop;  // padded coordinate of the seam's first sample
-  const long long o = ((long long)b * (nwg - 1) + j) * NFFT;
-  const bool table = NFFT % hop == 0;
-  for (int m = threadIdx.x; m < NFFT - hop; m += blockDim.x) {
-    const int sp = base + m, s = sp - NFFT / 2;
-    if (s < 0 || s >= L) continue;
-    const float a = seamR[o + m] + seamL[o + m];
-    const int q = sp / hop;
-    const int fmin = (sp - NFFT) >= 0 ? (sp - NFFT) / hop + 1 : 0;
-    const int fmax = min(q, T - 1);
-    float wss;
-    if (table && fmin == q - NFFT / hop + 1 && fmax == q) {
-      wss = wssr[sp - q * hop];
+    const float v = wss > 1.17549435e-38f ? acc[i] * __builtin_amdgcn_rcpf(wss) : acc[i];
+    const bool right = F1 < T && fmax >= F1;  // shared with the next workgroup
+    if ((F0 > 0 && fmin < F0) || right) {
+      // a seam sample: exactly two workgroups add into a zeroed word, and a + b = b + a in
+      // IEEE arithmetic, so the result does not depend on which arrives first
+      unsafeAtomicAdd(yr + s, v);
+      if (right && yn) yn[s] = 0.f;  // the next synthesis target's seam starts from zero
     } else {
-      wss = 0.f;
-      for (int fr = fmin; fr <= fmax; ++fr) wss += h2g[sp - fr * hop];
+      yr[s] = v;
     }
-    y[(long long)b * L + s] = wss > 1.17549435e-38f ? a * __builtin_amdgcn_rcpf(wss) : a;
   }
 }
 
@@ -1643,8 +1599,9 @@ int istft2_launch(const float2* cur, const float2* prev, const float* mag, float
   return MST_OK;
 }
 
-// One-pass Griffin-Lim synthesis (gl_synth_kernel + gl_seam_kernel); seams: B (nwg - 1) NFFT
-// floats each for the left and right partial sums; tables: Hann^2 and the interior wss.
+// One-pass Griffin-Lim synthesis (gl_synth_kernel). Seam samples (shared by two workgroups) are
+// added atomically into y, whose seams must be zero on entry; the launch zeroes the seams of
+// `ynext` (the next synthesis target) as it goes.
 static bool gl_one_pass(int hop) {
   static const bool two = [] {  // MST_GL_TWO_PASS=1: the frames-workspace path (A/B tuning)
     const char* e = getenv("MST_GL_TWO_PASS");
@@ -1654,23 +1611,13 @@ static bool gl_one_pass(int hop) {
 }
 
 int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, float beta,
-                    int normalize, int B, int T, int hop, float* seamL, float* seamR,
-                    const float* tabs, float* y, hipStream_t st) {
+                    int normalize, int B, int T, int hop, float* y, float* ynext, hipStream_t st) {
   const int G = gl_frames(hop);
   const int nwg = ceil_div(T, G);
   hipLaunchKernelGGL(gl_synth_kernel, dim3(nwg, B), dim3(64 * GLW), 0, st, cur, prev, mag, beta,
-                     normalize, T, hop, G, nwg, y, seamL, seamR);
+                     normalize, T, hop, G, nwg, y, ynext);
   MST_CHECK_LAUNCH();
-  if (nwg > 1) {
-    hipLaunchKernelGGL(gl_seam_kernel, dim3(nwg - 1, B), dim3(256), 0, st, seamL, seamR, T, hop, G,
-                       nwg, tabs, tabs + NFFT, y);
-    MST_CHECK_LAUNCH();
-  }
   return MST_OK;
-}
-
-static size_t gl_seam_floats(int B, int T, int hop) {
-  return (size_t)B * (ceil_div(T, gl_frames(hop)) - 1) * NFFT;
 }
 
 }  // namespace
@@ -1728,11 +1675,10 @@ size_t mst_griffinlim_workspace_size(int32_t B, int32_t F, int32_t T, int32_t ho
   const int CB = gl_chunk(B, F, T, hop);
   size_t bins = (size_t)B * F * T, cbins = (size_t)CB * F * T;
   size_t L = (size_t)hop * (T - 1);
-  // St (real, all clips) + two complex spectra + signal + windowed frames of one chunk, each
-  // rounded to 256 B
+  // St (real, all clips) + two complex spectra + two signals + windowed frames of one chunk,
+  // each rounded to 256 B
   auto r = [](size_t n) { return (n + 255) / 256 * 256; };
-  return r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4) +
-         2 * r(gl_seam_floats(CB, T, hop) * 4) + r((NFFT + 1024) * 4);
+  return r(bins * 4) + 2 * r(cbins * 8) + 2 * r((size_t)CB * L * 4) + r((size_t)CB * T * NFFT * 4);
 }
 
 int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t hop, int32_t n_iter,
@@ -1752,18 +1698,13 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   float2* R1 = (float2*)(w + r(bins * 4) + r(cbins * 8));
   float* sig = (float*)(w + r(bins * 4) + 2 * r(cbins * 8));
   const int L = hop * (T - 1);
-  float* frames = (float*)(w + r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4));
-  float* seamL = (float*)((char*)frames + r((size_t)CB * T * NFFT * 4));
-  float* seamR = (float*)((char*)seamL + r(gl_seam_floats(CB, T, hop) * 4));
-  float* tabs = (float*)((char*)seamR + r(gl_seam_floats(CB, T, hop) * 4));
+  float* sig2 = (float*)(w + r(bins * 4) + 2 * r(cbins * 8) + r((size_t)CB * L * 4));
+  float* frames = (float*)((char*)sig2 + r((size_t)CB * L * 4));
   const bool one = gl_one_pass(hop);
-  if (one) {
-    hipLaunchKernelGGL(gl_tables_kernel, dim3(1), dim3(256), 0, st, hop, tabs, tabs + NFFT);
-    MST_CHECK_LAUNCH();
-  }
   const float beta = momentum / (1.f + momentum);
-  auto synth = [&](const float2* c, const float2* p, const float* m, int nb, float* out) {
-    return one ? gl_synth_launch(c, p, m, beta, c != nullptr, nb, T, hop, seamL, seamR, tabs, out, st)
+  // synthesis into `out`; the one-pass kernel also zeroes the seams of `next` (the target after it)
+  auto synth = [&](const float2* c, const float2* p, const float* m, int nb, float* out, float* next) {
+    return one ? gl_synth_launch(c, p, m, beta, c != nullptr, nb, T, hop, out, next, st)
                : istft2_launch(c, p, m, beta, c != nullptr, nb, T, hop, frames, out, st);
   };
   {
@@ -1774,6 +1715,14 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
   for (int c0 = 0; c0 < B; c0 += CB) {
     const int nb = min(CB, B - c0);
     const float* Sc = St + (size_t)c0 * F * T;
+    float* yc = y + (size_t)c0 * L;
+    // synthesis targets alternate sig, sig2 and end in the caller's y
+    float* outs[2] = {sig, sig2};
+    auto target = [&](int it) { return it < n_iter ? outs[it & 1] : yc; };
+    if (one) {
+      const hipError_t e = hipMemsetAsync(target(0), 0, (size_t)nb * L * 4, st);
+      if (e != hipSuccess) return -(int)e;
+    }
     // iteration 0 uses the initial phases; iteration 1 has no momentum term (tprev = 0)
     const float2* cur =
         angles0 ? reinterpret_cast<const float2*>(angles0) + (size_t)c0 * F * T : nullptr;
@@ -1781,15 +1730,15 @@ int mst_griffinlim_f32(const float* S, int32_t B, int32_t F, int32_t T, int32_t 
     float2* bufs[2] = {R0, R1};
     int rc;
     for (int it = 0; it < n_iter; ++it) {
-      rc = synth(cur, prev, Sc, nb, sig);
+      rc = synth(cur, prev, Sc, nb, target(it), target(it + 1));
       if (rc) return rc;
       float2* nxt = bufs[it & 1];
-      rc = stft_launch(MODE_COMPLEX, sig, nb, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
+      rc = stft_launch(MODE_COMPLEX, target(it), nb, L, NFFT, hop, MST_PAD_REFLECT, (float*)nxt, MelTab{}, st);
       if (rc) return rc;
       prev = (it == 0) ? nullptr : cur;
       cur = nxt;
     }
-    rc = synth(cur, prev, Sc, nb, y + (size_t)c0 * L);
+    rc = synth(cur, prev, Sc, nb, yc, nullptr);
     if (rc) return rc;
   }
   return MST_OK;

@@ -455,8 +455,11 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
             const c2 P = (zf + conjc(zr)) * 0.5f;
             const c2 D = zf - conjc(zr);
             const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
-            const float sp = sqrtf(P.x * P.x + P.y * P.y), st = sqrtf(Q.x * Q.x + Q.y * Q.y);
-            const float lp = logf(sp + a.eps), lt = logf(st + a.eps);
+            // hardware sqrt / log2 / rcp (1 ulp): the library forms add ~10 instructions each
+            const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
+            const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
+            const float lp = __log2f(sp + a.eps) * 0.69314718055994531f;
+            const float lt = __log2f(st + a.eps) * 0.69314718055994531f;
             if (t >= f_own0) {
               s_abs += fabsf(sp - st);
               s_log += fabsf(lp - lt);
@@ -464,7 +467,7 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
             if (grad && sp > 0.f) {
               const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
               const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
-              zg = P * (g / sp);
+              zg = P * (g * __builtin_amdgcn_rcpf(sp));
             }
           }
           if (pass == 0) zga[jj] = zg;
