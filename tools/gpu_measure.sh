@@ -54,6 +54,21 @@ for what in "$@"; do
     profaux)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profaux" -o run -- \
         python3 bench_aux.py --no-cpu-baseline --steps 5 --warmup 2 > "$OUT/profaux.json" 2> "$OUT/profaux.err" ;;
+    abstft)
+      for v in 2 4; do
+        MST_STFT_WAVE=$v timeout -k 10 300 python -u -m pytest tests/test_gpu_spectral.py -x -v --timeout 120 \
+          --timeout-method thread -k "stft or logpow or power" > "$OUT/pytest_stftwave$v.log" 2>&1
+      done
+      for v in 0 2 4 0 2 4; do
+        MST_STFT_WAVE=$v timeout -k 10 180 python -u bench_aux.py --workload frontend --no-cpu-baseline \
+          >> "$OUT/ab_stftwave$v.jsonl" 2>> "$OUT/ab_stft.err"
+      done ;;
+    abmss2)
+      for lib in "" variants/mss_head/libmst_hip.so "" variants/mss_head/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_mss2.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 \
+          >> "$OUT/ab_mss2.jsonl" 2>> "$OUT/ab_mss2.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
