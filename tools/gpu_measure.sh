@@ -69,6 +69,13 @@ for what in "$@"; do
         MST_LIB_PATH=$lib timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 \
           >> "$OUT/ab_mss2.jsonl" 2>> "$OUT/ab_mss2.err"
       done ;;
+    abpk)
+      MST_STFT_PK=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_spectral.py tests/test_gpu_inference.py -x -v --timeout 120 \
+        --timeout-method thread > "$OUT/pytest_pk.log" 2>&1
+      for v in 0 1 0 1; do
+        MST_STFT_PK=$v timeout -k 10 180 python -u bench_aux.py --workload frontend --no-cpu-baseline \
+          >> "$OUT/ab_pk$v.jsonl" 2>> "$OUT/ab_pk.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
