@@ -107,7 +107,7 @@ def _measured_traffic(kernel_key):
 
 def _gl_traffic(n_iter):
     """HBM bytes of one Griffin-Lim call from the newest round's PMC passes over the Griffin-Lim
-    leg (profiles/r*/gl_traffic.json): (n_iter + 1) syntheses (+ seam passes before round 3), n_iter complex
+    leg (profiles/r*/gl_traffic.json): (n_iter + 1) syntheses (+ seam passes in earlier builds), n_iter complex
     STFTs and the one magnitude transpose, each 2 x FETCH_SIZE + WRITE_SIZE per launch."""
     pdir = os.path.join(ROOT, "profiles")
     for r in sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) if os.path.isdir(pdir) else []:

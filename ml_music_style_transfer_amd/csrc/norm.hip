@@ -6,45 +6,56 @@
 //   lrelu(lastconv) + L1 loss fwd/bwd   model/model.py:299, model/train.py:132-135,140
 //   Adam over the flat parameter buffer  model/train.py:188,143
 //   piano-roll binarise + onset/offset   preprocessing/preprocess.py:148-155
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
 
 // ---------------------------------------------------------------------------
-// InstanceNorm + LeakyReLU (+ MaxPool) forward. One wave per row; lane l holds the
-// element pairs (2l + 128p, 2l + 128p + 1), p < NP, so the pool pairs are lane-local.
+// InstanceNorm + LeakyReLU (+ MaxPool) forward. G lanes per row (a wave, or for short rows
+// (T <= 2 G < 128) a G-lane segment of one, so several rows share a wave); lane l holds the
+// element pairs (2l + 2Gp, 2l + 2Gp + 1), p < NP, so the pool pairs are lane-local.
 // Two-pass (exact) mean/variance in registers; biased variance like torch.
 // ---------------------------------------------------------------------------
-template <int NP>
+// sum over the G-lane segment of a wave (G = 64: wave_sum's order)
+template <int G>
+__device__ __forceinline__ float seg_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+template <int NP, int G>
 __global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y, long long rows,
                                                      int T, float eps, float slope,
                                                      float* __restrict__ a, float* __restrict__ pooled,
                                                      float* __restrict__ mean,
                                                      float* __restrict__ rstd) {
-  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int lane = threadIdx.x & (G - 1);
   if (row >= rows) return;
   const float* yr = y + row * T;
   float e0[NP], e1[NP];
   float s = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 128 * q;
+    int i0 = 2 * lane + 2 * G * q;
     e0[q] = i0 < T ? yr[i0] : 0.f;
     e1[q] = i0 + 1 < T ? yr[i0 + 1] : 0.f;
     s += e0[q] + e1[q];
   }
-  s = wave_sum(s);
+  s = seg_sum<G>(s);
   const float mu = s / (float)T;
   float v = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 128 * q;
+    int i0 = 2 * lane + 2 * G * q;
     float d0 = e0[q] - mu, d1 = e1[q] - mu;
     if (i0 < T) v += d0 * d0;
     if (i0 + 1 < T) v += d1 * d1;
   }
-  v = wave_sum(v);
+  v = seg_sum<G>(v);
   const float r = 1.f / sqrtf(v / (float)T + eps);
   if (lane == 0) {
     mean[row] = mu;
@@ -55,7 +66,7 @@ __global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y
   float* pr = pooled ? pooled + row * Tp : nullptr;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 128 * q;
+    int i0 = 2 * lane + 2 * G * q;
     float a0 = lrelu((e0[q] - mu) * r, slope);
     float a1 = lrelu((e1[q] - mu) * r, slope);
     if (i0 < T) ar[i0] = a0;
@@ -103,7 +114,7 @@ __global__ __launch_bounds__(256) void in_fwd_long_kernel(const float* __restric
 
 // Backward: da = d_a + unpool(d_pool0 + d_pool1) (to the pair's argmax), dz = lrelu'(z) da,
 // dy = rstd * (dz - mean(dz) - z * mean(dz * z)).
-template <int NP>
+template <int NP, int G>
 __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
@@ -113,8 +124,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
                                                      const float* __restrict__ dp1,
                                                      float* __restrict__ dy,
                                                      float* __restrict__ rowsum) {
-  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const int lane = threadIdx.x & (G - 1);
   if (row >= rows) return;
   const float* yr = y + row * T;
   const float mu = mean[row], r = rstd[row];
@@ -123,7 +134,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 128 * q;
+    int i0 = 2 * lane + 2 * G * q;
     bool ok0 = i0 < T, ok1 = i0 + 1 < T;
     float y0 = ok0 ? yr[i0] : mu, y1 = ok1 ? yr[i0 + 1] : mu;
     z0[q] = (y0 - mu) * r;
@@ -145,13 +156,13 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
     s1 += g0[q] + g1[q];
     s2 += g0[q] * z0[q] + g1[q] * z1[q];
   }
-  s1 = wave_sum(s1) / (float)T;
-  s2 = wave_sum(s2) / (float)T;
+  s1 = seg_sum<G>(s1) / (float)T;
+  s2 = seg_sum<G>(s2) / (float)T;
   float* dr = dy + row * T;
   float rs = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 128 * q;
+    int i0 = 2 * lane + 2 * G * q;
     if (i0 < T) {
       const float v = r * (g0[q] - s1 - z0[q] * s2);
       dr[i0] = v;
@@ -164,7 +175,7 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
     }
   }
   if (rowsum) {
-    rs = wave_sum(rs);
+    rs = seg_sum<G>(rs);
     if (lane == 0) rowsum[row] = rs;
   }
 }
@@ -393,6 +404,19 @@ __global__ void relu_gate_bwd_kernel(const float* __restrict__ d, const float* _
     out[i] = h[i] > 0.f ? d[i] * s : 0.f;
 }
 
+// lanes per InstanceNorm row: two elements per lane, a power of two in [4, 64] (short rows share
+// a wave instead of leaving most of its lanes idle); MST_IN_SEG=0 keeps one row per wave (A/B)
+int in_lanes(int T) {
+  static const bool seg = [] {
+    const char* e = getenv("MST_IN_SEG");
+    return !(e && e[0] == '0');
+  }();
+  if (!seg) return 64;
+  int g = 4;
+  while (g < 64 && 2 * g < T) g *= 2;
+  return g;
+}
+
 int grid_for(long long n, int per = 256, int cap = 8192) {
   long long g = (n + per - 1) / per;
   if (g > cap) g = cap;
@@ -409,10 +433,19 @@ int mst_instnorm_lrelu_fwd_f32(const float* y, int64_t rows, int32_t T, float ep
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
-  if (np <= 1) hipLaunchKernelGGL(in_fwd_kernel<1>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
-  else if (np <= 2) hipLaunchKernelGGL(in_fwd_kernel<2>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
-  else if (np <= 4) hipLaunchKernelGGL(in_fwd_kernel<4>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
-  else if (np <= 8) hipLaunchKernelGGL(in_fwd_kernel<8>, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
+  const int g = in_lanes(T);
+  dim3 gs((unsigned)((rows * g + 255) / 256));
+#define MST_IN(NP_, G_, GR) hipLaunchKernelGGL((in_fwd_kernel<NP_, G_>), GR, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd)
+  if (np <= 1 && g < 64) {
+    if (g == 4) MST_IN(1, 4, gs);
+    else if (g == 8) MST_IN(1, 8, gs);
+    else if (g == 16) MST_IN(1, 16, gs);
+    else MST_IN(1, 32, gs);
+  } else if (np <= 1) MST_IN(1, 64, grid);
+  else if (np <= 2) MST_IN(2, 64, grid);
+  else if (np <= 4) MST_IN(4, 64, grid);
+  else if (np <= 8) MST_IN(8, 64, grid);
+#undef MST_IN
   else hipLaunchKernelGGL(in_fwd_long_kernel, grid, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd);
   MST_CHECK_LAUNCH();
   return MST_OK;
@@ -425,10 +458,19 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
-  if (np <= 1) hipLaunchKernelGGL(in_bwd_kernel<1>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
-  else if (np <= 2) hipLaunchKernelGGL(in_bwd_kernel<2>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
-  else if (np <= 4) hipLaunchKernelGGL(in_bwd_kernel<4>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
-  else if (np <= 8) hipLaunchKernelGGL(in_bwd_kernel<8>, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
+  const int g = in_lanes(T);
+  dim3 gs((unsigned)((rows * g + 255) / 256));
+#define MST_IN(NP_, G_, GR) hipLaunchKernelGGL((in_bwd_kernel<NP_, G_>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum)
+  if (np <= 1 && g < 64) {
+    if (g == 4) MST_IN(1, 4, gs);
+    else if (g == 8) MST_IN(1, 8, gs);
+    else if (g == 16) MST_IN(1, 16, gs);
+    else MST_IN(1, 32, gs);
+  } else if (np <= 1) MST_IN(1, 64, grid);
+  else if (np <= 2) MST_IN(2, 64, grid);
+  else if (np <= 4) MST_IN(4, 64, grid);
+  else if (np <= 8) MST_IN(8, 64, grid);
+#undef MST_IN
   else hipLaunchKernelGGL(in_bwd_long_kernel, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
   MST_CHECK_LAUNCH();
   return MST_OK;

@@ -311,8 +311,11 @@ def test_linear_relu_dropout_gate(cuda):
 
 
 @pytest.mark.parametrize("T,pool", [(13, True), (252, True), (63, True), (860, True), (1500, True),
-                                    (2, False), (31, False)])
+                                    (2, False), (31, False), (15, True), (126, True), (5, False),
+                                    (64, True)])
 def test_instnorm_lrelu_pool(cuda, T, pool):
+    """Rows of T <= 128 share a wave in G-lane segments (G = 4 .. 32; norm.hip in_lanes), so the
+    cases cover every segment width, odd T, and a row count (15) that leaves a partial wave."""
     from ml_music_style_transfer_amd import kernels as K
     B, C = 3, 5
     y = _r(B, C, T, seed=27) * 3 + 0.5

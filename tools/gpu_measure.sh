@@ -76,6 +76,20 @@ for what in "$@"; do
         MST_STFT_PK=$v timeout -k 10 180 python -u bench_aux.py --workload frontend --no-cpu-baseline \
           >> "$OUT/ab_pk$v.jsonl" 2>> "$OUT/ab_pk.err"
       done ;;
+    abtau)
+      for t in 3.4e-6 2.6e-6 4.2e-6 3.4e-6 2.6e-6 4.2e-6; do
+        echo "== tau $t" >> "$OUT/ab_tau.jsonl"
+        MST_SPLITK_TAU=$t timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_tau.jsonl" 2>> "$OUT/ab_tau.err"
+      done ;;
+    abin)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -x -v --timeout 120 --timeout-method thread \
+        -k "instnorm" > "$OUT/pytest_in.log" 2>&1
+      for v in 0 1 0 1; do
+        echo "== MST_IN_SEG=$v" >> "$OUT/ab_in.jsonl"
+        MST_IN_SEG=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_in.jsonl" 2>> "$OUT/ab_in.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
