@@ -90,6 +90,12 @@ for what in "$@"; do
         MST_IN_SEG=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_in.jsonl" 2>> "$OUT/ab_in.err"
       done ;;
+    abgl)
+      for lib in "" variants/gl_head/libmst_hip.so "" variants/gl_head/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_gl.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
+          >> "$OUT/ab_gl.jsonl" 2>> "$OUT/ab_gl.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
