@@ -117,13 +117,15 @@ def _gl_traffic(n_iter):
         d = json.load(open(tj))
         per = {}
         for k, v in d.get("per_kernel", {}).items():
-            for key in ("gl_synth_kernel", "gl_seam_kernel", "stft_kernel<3>", "transpose_mag_kernel"):
+            for key in ("gl_synth_kernel", "gl_seam_kernel", "stft_kernel<3>", "transpose_mag_kernel",
+                        "fillBufferAligned"):
                 if key in k:
                     per[key] = 2 * v["fetch_raw_per_launch"] + v["write_per_launch"]
         if "gl_synth_kernel" not in per or "stft_kernel<3>" not in per:
             continue
         tot = ((n_iter + 1) * (per["gl_synth_kernel"] + per.get("gl_seam_kernel", 0.0))
-               + n_iter * per["stft_kernel<3>"] + per.get("transpose_mag_kernel", 0.0))
+               + n_iter * per["stft_kernel<3>"] + per.get("transpose_mag_kernel", 0.0)
+               + per.get("fillBufferAligned", 0.0))  # the seam-zeroing memset (atomic-seam builds)
         return round(tot), f"profiles/{r}/gl_traffic.json ({d.get('build', '')})"
     return None, None
 

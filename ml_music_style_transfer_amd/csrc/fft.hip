@@ -12,7 +12,7 @@
 // kernels below use fft1024_v2 instead (0 conflicts, profiles/r02). This round-1 path remains for
 // the frame-major complex STFT (Griffin-Lim) and the iSTFT. Twiddles come from a 512-entry quarter-wave LDS table
 // (W^(512q + r) = (-i)^q W^r), built in double precision on the host side of the
-// compiler (constexpr-free: computed once per workgroup with sincospi in f64).
+// compiler (constexpr tables, copied to LDS per workgroup).
 //
 // STFT workgroups: 512 threads (8 waves) x 32 frames of one clip. Results are staged
 // through LDS (reusing the FFT scratch) so each (bin, 32 frames) row of the (B, F, T)
@@ -60,12 +60,69 @@ __device__ __forceinline__ c2 tw(const c2* qt, int k) {
   return o;
 }
 
-__device__ void build_qtable(c2* qt) {
-  for (int r = threadIdx.x; r < QT; r += blockDim.x) {
-    double s, c;
-    sincospi((double)r / 1024.0, &s, &c);
-    qt[r] = mk((float)c, (float)-s);
+// cos / sin of 2 pi m / n in double, evaluated at compile time (quadrant-reduced Taylor series)
+constexpr double kPiD = 3.14159265358979323846264338327950288;
+constexpr void cx_sincos_turn(long long m, long long n, double& c, double& s) {
+  m %= n;
+  if (m < 0) m += n;
+  const long long q = (4 * m) / n;                 // quadrant
+  const double x = (double)(4 * m - q * n) / (double)n * (kPiD / 2);  // [0, pi/2)
+  double x2 = x * x, ts = x, ss = x, tc = 1.0, sc = 1.0;
+  for (int k = 1; k < 16; ++k) {
+    ts *= -x2 / ((2.0 * k) * (2.0 * k + 1.0));
+    ss += ts;
+    tc *= -x2 / ((2.0 * k - 1.0) * (2.0 * k));
+    sc += tc;
   }
+  const double cq[4] = {sc, -ss, -sc, ss}, sq[4] = {ss, sc, -ss, -sc};
+  c = cq[q];
+  s = sq[q];
+}
+struct FftTabs {
+  float2 a[15 * 64];  // a[(k1 - 1) 64 + l] = W1024^(l k1)
+  float2 b[3 * 16];   // b[(q - 1) 16 + l]  = W64^(l q)
+  float2 p[512];      // p[k] = W2048^k
+};
+constexpr FftTabs make_tabs() {
+  FftTabs t{};
+  double c = 0, s = 0;
+  for (int k1 = 1; k1 < 16; ++k1)
+    for (int l = 0; l < 64; ++l) {
+      cx_sincos_turn((long long)l * k1, 1024, c, s);
+      t.a[(k1 - 1) * 64 + l] = float2{(float)c, (float)-s};
+    }
+  for (int q = 1; q < 4; ++q)
+    for (int l = 0; l < 16; ++l) {
+      cx_sincos_turn((long long)l * q, 64, c, s);
+      t.b[(q - 1) * 16 + l] = float2{(float)c, (float)-s};
+    }
+  for (int k = 0; k < 512; ++k) {
+    cx_sincos_turn(k, 2048, c, s);
+    t.p[k] = float2{(float)c, (float)-s};
+  }
+  return t;
+}
+__device__ constexpr FftTabs kFftTabs = make_tabs();
+constexpr int TAB_F4 = (int)(sizeof(FftTabs) / 16);
+// W4096^(2 l + 1) = (cos, -sin)(pi (2 l + 1) / 2048), l < 64: the window phase of the odd samples
+struct EhTab {
+  float2 e[64];
+};
+constexpr EhTab make_eh() {
+  EhTab t{};
+  double c = 0, s = 0;
+  for (int l = 0; l < 64; ++l) {
+    cx_sincos_turn(2 * l + 1, 4096, c, s);
+    t.e[l] = float2{(float)c, (float)-s};
+  }
+  return t;
+}
+__device__ constexpr EhTab kEh = make_eh();
+
+// quarter-wave table qt[r] = W2048^r, r < 512: copied from the compile-time table (no f64
+// sincospi per workgroup)
+__device__ void build_qtable(c2* qt) {
+  for (int r = threadIdx.x; r < QT; r += blockDim.x) qt[r] = mk(kFftTabs.p[r].x, kFftTabs.p[r].y);
 }
 
 template <bool INV>
@@ -302,11 +359,7 @@ __global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ 
   const int f0 = blockIdx.x * FR;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   build_qtable(qt);
-  if (threadIdx.x < 64) {
-    double sn, cs;
-    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
-    eht[threadIdx.x] = mk((float)cs, (float)-sn);
-  }
+  if (threadIdx.x < 64) eht[threadIdx.x] = mk(kEh.e[threadIdx.x].x, kEh.e[threadIdx.x].y);
   __syncthreads();
   const float* xr = x + (long long)b * L;
   c2* S = scratch + wave * SCR;
@@ -441,50 +494,6 @@ __global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ 
 #endif
 constexpr int RSTR_MEL = 130;      // staging row stride for <= 128 mel bands (= 2 mod 32)
 
-// cos / sin of 2 pi m / n in double, evaluated at compile time (quadrant-reduced Taylor series)
-constexpr double kPiD = 3.14159265358979323846264338327950288;
-constexpr void cx_sincos_turn(long long m, long long n, double& c, double& s) {
-  m %= n;
-  if (m < 0) m += n;
-  const long long q = (4 * m) / n;                 // quadrant
-  const double x = (double)(4 * m - q * n) / (double)n * (kPiD / 2);  // [0, pi/2)
-  double x2 = x * x, ts = x, ss = x, tc = 1.0, sc = 1.0;
-  for (int k = 1; k < 16; ++k) {
-    ts *= -x2 / ((2.0 * k) * (2.0 * k + 1.0));
-    ss += ts;
-    tc *= -x2 / ((2.0 * k - 1.0) * (2.0 * k));
-    sc += tc;
-  }
-  const double cq[4] = {sc, -ss, -sc, ss}, sq[4] = {ss, sc, -ss, -sc};
-  c = cq[q];
-  s = sq[q];
-}
-struct FftTabs {
-  float2 a[15 * 64];  // a[(k1 - 1) 64 + l] = W1024^(l k1)
-  float2 b[3 * 16];   // b[(q - 1) 16 + l]  = W64^(l q)
-  float2 p[512];      // p[k] = W2048^k
-};
-constexpr FftTabs make_tabs() {
-  FftTabs t{};
-  double c = 0, s = 0;
-  for (int k1 = 1; k1 < 16; ++k1)
-    for (int l = 0; l < 64; ++l) {
-      cx_sincos_turn((long long)l * k1, 1024, c, s);
-      t.a[(k1 - 1) * 64 + l] = float2{(float)c, (float)-s};
-    }
-  for (int q = 1; q < 4; ++q)
-    for (int l = 0; l < 16; ++l) {
-      cx_sincos_turn((long long)l * q, 64, c, s);
-      t.b[(q - 1) * 16 + l] = float2{(float)c, (float)-s};
-    }
-  for (int k = 0; k < 512; ++k) {
-    cx_sincos_turn(k, 2048, c, s);
-    t.p[k] = float2{(float)c, (float)-s};
-  }
-  return t;
-}
-__device__ constexpr FftTabs kFftTabs = make_tabs();
-constexpr int TAB_F4 = (int)(sizeof(FftTabs) / 16);
 
 __device__ __forceinline__ void swap32(c2& lo, c2& hi) {  // lane bit 5 <-> the lo/hi pair
   auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(lo.x), __float_as_uint(hi.x), false, false);
@@ -1001,11 +1010,7 @@ __global__ __launch_bounds__(512, 2) void istft_kernel(const float2* __restrict_
   const int s0 = blockIdx.x * ISEG;  // segment start (unpadded coords)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   build_qtable(qt);
-  if (threadIdx.x < 64) {
-    double sn, cs;
-    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
-    eht[threadIdx.x] = mk((float)cs, (float)-sn);
-  }
+  if (threadIdx.x < 64) eht[threadIdx.x] = mk(kEh.e[threadIdx.x].x, kEh.e[threadIdx.x].y);
   __syncthreads();
   const int K = NFFT / hop;  // frames covering an interior sample (when hop divides NFFT)
   const bool table = (NFFT % hop) == 0 && hop <= 512;
@@ -1169,11 +1174,7 @@ __global__ __launch_bounds__(256, 4) void ifft_frames_kernel(const float2* __res
   const int b = blockIdx.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   build_qtable(qt);
-  if (threadIdx.x < 64) {
-    double sn, cs;
-    sincospi((2.0 * threadIdx.x + 1.0) / 2048.0, &sn, &cs);
-    eht[threadIdx.x] = mk((float)cs, (float)-sn);
-  }
+  if (threadIdx.x < 64) eht[threadIdx.x] = mk(kEh.e[threadIdx.x].x, kEh.e[threadIdx.x].y);
   __syncthreads();
   c2* S = scratch + wave * SCR;
   const bool norm = normalize != 0;
@@ -1409,12 +1410,7 @@ __global__ __launch_bounds__(512, 4) void gl_synth_kernel(const float2* __restri
   for (int i = 0; i < GL_OWN; ++i) acc[i] = 0.f;
   const float inv_hop = 1.f / (float)hop;
   const bool has_c = cur != nullptr, has_p = prev != nullptr, norm = normalize != 0;
-  c2 eh;  // W4096^(2 lane + 1): the window phase of the odd samples
-  {
-    double sn, cs;
-    sincospi((2.0 * (threadIdx.x & 63) + 1.0) / 2048.0, &sn, &cs);
-    eh = mk((float)cs, (float)-sn);
-  }
+  const c2 eh = mk(kEh.e[threadIdx.x & 63].x, kEh.e[threadIdx.x & 63].y);  // W4096^(2 lane + 1)
   GlRaw rb;
   gl_issue(cur, prev, b, T, F0 + wave, F0 + wave < F1, threadIdx.x & 63, rb);
 #pragma unroll 1
