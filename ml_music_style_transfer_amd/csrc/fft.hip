@@ -624,6 +624,29 @@ __device__ __forceinline__ void power_pairs_v2(const c2 v[16], const FftTabs& tb
   r[16] = LOG ? ln_1p_quarter(z4) : 0.25f * z4;
 }
 
+// Complex bins from Z[lane + 64 j] in v, in power_pairs_v2's pairing: x[2j] = X[l + 64 j],
+// x[2j + 1] = X[1024 - l - 64 j] (j = 0..7; lane 0, j = 0: X[1024]), x[16] = X[512] (lane 0).
+__device__ __forceinline__ void complex_pairs_v2(const c2 v[16], const FftTabs& tb, int lane,
+                                                 c2 x[17]) {
+  const int src = ((64 - lane) & 63) * 4;
+  c2 prev = v[0];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const c2 bpj = mk(bperm(src, v[15 - j].x), bperm(src, v[15 - j].y));
+    const c2 Bq = lane == 0 ? prev : bpj;
+    prev = bpj;
+    const c2 A = v[j];
+    const c2 E = mk(A.x + Bq.x, A.y - Bq.y);
+    const c2 D = mk(A.y + Bq.y, Bq.x - A.x);
+    const float2 w = tb.p[lane + 64 * j];
+    const c2 TD = cmul(mk(w.x, w.y), D);
+    const c2 P = E + TD, M = E - TD;  // 2 X[k], 2 conj X[1024 - k]
+    x[2 * j] = mk(0.5f * P.x, 0.5f * P.y);
+    x[2 * j + 1] = mk(0.5f * M.x, -0.5f * M.y);
+  }
+  x[16] = mk(v[8].x, -v[8].y);  // X[512] = conj Z[512]
+}
+
 // staging position of (frame row, bin k < 1024): row stride 1024, bits of k XORed with the row's
 // quad index so the write-out's 4-row column gathers are bank-conflict-free (16 rows: 8 bins x
 // 4 quads per 32 lanes, XOR 8 q; 8 rows: 16 bins x 2 quads, XOR 16 q)
@@ -792,8 +815,9 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
   float* span = reinterpret_cast<float*>(reinterpret_cast<char*>(scratch) + SPAN_OFF);
   const int sp = (FPB - 1) * hop + NFFT;  // span samples (launcher: fits after the staging)
   constexpr bool MELM = MODE == MODE_MEL;
+  constexpr bool CPLX = MODE == MODE_COMPLEX;  // frame-major (B, T, F, 2): stored from registers
   const int nrows = MELM ? mel.n_mels : NB;
-  const int clip_bytes = nrows * T * 4;  // < 2^31: checked by the launcher
+  const int clip_bytes = CPLX ? NB * T * 8 : nrows * T * 4;  // < 2^31: checked by the launcher
   // this lane's 32 window weights (Hann at samples 2n, 2n + 1, n = lane + 64 j), kept in
   // registers for the whole kernel (80 -> 112 VGPRs, still 4 waves per SIMD): 32 multiplies
   // per frame instead of ~110 instructions recomputing them
@@ -814,7 +838,7 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
   const long long rowT = T;
   auto clip_of = [&](int u) { return xg + 8 * (u / nblk); };
   auto frame0_of = [&](int u) { return (u % nblk) * FPB; };
-  constexpr int NST = MELM ? 1 : 5;  // write-out stores per thread per block (V4)
+  constexpr int NST = CPLX ? 17 : (MELM ? 1 : 5);  // write-out stores per thread per block (V4)
   constexpr int VM_NST = 0x0f70 | (NST & 15);  // s_waitcnt vmcnt(NST), expcnt/lgkmcnt unmasked
 
   load_span<FMW>(x + (long long)clip_of(wi) * L, L, frame0_of(wi) * hop - NFFT / 2, sp, pad_mode, span,
@@ -850,12 +874,15 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
     LDS_BARRIER();  // the span is read: the FFT scratch may overwrite it
     STAMP(1);
     float res[17];
+    c2 xc[17];  // CPLX: this lane's complex bins
     if (fl < nfr) {
       c2 v[16];
 #pragma unroll
       for (int j = 0; j < 16; ++j) v[j] = mk(raw[j].x * wwe[j], raw[j].y * wwo[j]);
       fft1024_v2(v, S, tbl, lane);
-      if (!MELM) {
+      if (CPLX) {
+        complex_pairs_v2(v, tbl, lane, xc);
+      } else if (!MELM) {
         power_pairs_v2<MODE == MODE_LOGPOW>(v, tbl, lane, res);
       } else {
         float r[17];
@@ -893,6 +920,24 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
                   span, wave, lane);
     }
     STAMP(7);
+    if constexpr (CPLX) {
+      // frame-major rows are contiguous: each lane stores its 17 bins straight from registers
+      // (a fixed count of buffer stores, dropped for a frame past the clip), no staging
+      const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + (long long)b * T * NB * 2, (short)0,
+                                                       clip_bytes, 0x00020000);
+      const bool ok = fl < nfr;
+      const int fo = (f0 + fl) * NB;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int oa = ok ? (fo + lane + 64 * j) * 8 : clip_bytes;
+        const int ob = ok ? (fo + NC - lane - 64 * j) * 8 : clip_bytes;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_float2(xc[2 * j].x, xc[2 * j].y)), rs, oa, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_float2(xc[2 * j + 1].x, xc[2 * j + 1].y)), rs, ob, 0, 0);
+      }
+      const int om = (ok && lane == 0) ? (fo + NC / 2) * 8 : clip_bytes;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, make_float2(xc[16].x, xc[16].y)), rs, om, 0, 0);
+      continue;
+    }
     if (fl < nfr) {
       if (!MELM) {
 #pragma unroll
@@ -1535,16 +1580,25 @@ __global__ void transpose_mag_kernel(const float* __restrict__ S, int F, int T, 
   }
 }
 
+static bool stft_cx_fm() {  // MST_STFT_CX_FM=0: complex STFT on the round-1 kernel (A/B)
+  static const bool v = [] {
+    const char* e = getenv("MST_STFT_CX_FM");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int pad_mode, float* out,
                 MelTab mel, hipStream_t st) {
   MST_REQUIRE(x && out && B > 0 && n_fft == NFFT && hop > 0);
   MST_REQUIRE(L > NFFT / 2 || pad_mode == MST_PAD_CONSTANT);
   MST_REQUIRE(pad_mode == MST_PAD_REFLECT || pad_mode == MST_PAD_CONSTANT);
   const int T = 1 + L / hop;
-  if (mode == MODE_COMPLEX) {  // frame-major (B, T, F, 2): each frame's spectrum is contiguous
+  const bool fm_fits = !(hop & 1) && (long long)((FM_WAVES - 1) * hop + NFFT) * 4 <= (long long)FM_WAVES * (SCR * 8 - NC * 4);
+  if (mode == MODE_COMPLEX && !(fm_fits && stft_cx_fm())) {  // frame-major (B, T, F, 2), round-1 kernel
     dim3 grid(ceil_div(T, FR), B), block(512);
     hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel);
-  } else if ((hop & 1) || (long long)((FM_WAVES - 1) * hop + NFFT) * 4 > (long long)FM_WAVES * (SCR * 8 - NC * 4)) {
+  } else if (!fm_fits) {
     // odd hops (8-byte span reads) or spans beyond the scratch: the round-1 kernel
     dim3 grid(ceil_div(T, FR), B), block(512);
     switch (mode) {
@@ -1559,12 +1613,13 @@ int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int 
     const int W = (int)(per_group < wmax ? per_group : wmax);
     dim3 grid(8 * W), block(64 * FM_WAVES);
     const long long rows = mode == MODE_MEL ? mel.n_mels : NB;
-    MST_REQUIRE(rows * T * 4 < (1ll << 31));  // per-clip buffer descriptors
-    const bool v4 = (T & 3) == 0 && ((uintptr_t)out & 15) == 0;
+    MST_REQUIRE(rows * T * (mode == MODE_COMPLEX ? 8 : 4) < (1ll << 31));  // per-clip buffer descriptors
+    const bool v4 = mode == MODE_COMPLEX || ((T & 3) == 0 && ((uintptr_t)out & 15) == 0);
 #define MST_STFT_FM(M, V) hipLaunchKernelGGL((stft_fm_kernel<M, V, FM_WAVES>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W)
     switch (mode) {
       case MODE_LOGPOW: if (v4) MST_STFT_FM(MODE_LOGPOW, true); else MST_STFT_FM(MODE_LOGPOW, false); break;
       case MODE_POWER: if (v4) MST_STFT_FM(MODE_POWER, true); else MST_STFT_FM(MODE_POWER, false); break;
+      case MODE_COMPLEX: MST_STFT_FM(MODE_COMPLEX, true); break;
       default: if (v4) MST_STFT_FM(MODE_MEL, true); else MST_STFT_FM(MODE_MEL, false); break;
     }
 #undef MST_STFT_FM

@@ -46,7 +46,7 @@ for what in "$@"; do
         timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_legacy_nt512.json" 2>&1 ;;
     gltest)
       timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
-        -k "griffinlim or istft" > "$OUT/pytest_gl.log" 2>&1 ;;
+        -k "griffinlim or istft or stft or mel" > "$OUT/pytest_gl.log" 2>&1 ;;
     auxgl)
       timeout -k 10 300 python -u bench_aux.py --workload griffinlim --no-cpu-baseline > "$OUT/aux_gl.json" 2> "$OUT/aux_gl.err" ;;
     auxmss)
@@ -91,10 +91,18 @@ for what in "$@"; do
           >> "$OUT/ab_in.jsonl" 2>> "$OUT/ab_in.err"
       done ;;
     abgl)
-      for lib in "" variants/gl_head/libmst_hip.so "" variants/gl_head/libmst_hip.so; do
+      for lib in "" variants/gl_head/libmst_hip.so "" variants/gl_head/libmst_hip.so; do  # in-tree vs HEAD fft.hip
         echo "== lib ${lib:-in-tree}" >> "$OUT/ab_gl.jsonl"
         MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
           >> "$OUT/ab_gl.jsonl" 2>> "$OUT/ab_gl.err"
+      done ;;
+    abcx)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_spectral.py tests/test_istft_grad.py tests/test_gpu_inference.py \
+        -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_cx.log" 2>&1
+      for v in 1 0 1 0; do
+        echo "== MST_STFT_CX_FM=$v" >> "$OUT/ab_cx.jsonl"
+        MST_STFT_CX_FM=$v timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
+          >> "$OUT/ab_cx.jsonl" 2>> "$OUT/ab_cx.err"
       done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
