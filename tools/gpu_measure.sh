@@ -104,6 +104,14 @@ for what in "$@"; do
         MST_STFT_CX_FM=$v timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
           >> "$OUT/ab_cx.jsonl" 2>> "$OUT/ab_cx.err"
       done ;;
+    abgltab)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_spectral.py -x -v --timeout 120 --timeout-method thread \
+        -k "griffinlim" > "$OUT/pytest_gltab.log" 2>&1
+      for v in 1 0 1 0; do
+        echo "== MST_GL_TABS=$v" >> "$OUT/ab_gltab.jsonl"
+        MST_GL_TABS=$v timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
+          >> "$OUT/ab_gltab.jsonl" 2>> "$OUT/ab_gltab.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
