@@ -904,7 +904,20 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
           float acc = 0.f;
           if (m < mel.n_mels) {
             const int st = mel.start[m], n = mel.len[m], wo2 = mel.woff[m];
-            for (int i = 0; i < n; ++i) acc += mel.w[wo2 + i] * P[st + i];
+            // four interleaved partial sums: four weight loads and FMAs in flight per step instead
+            // of one serial chain over the band (up to 48-64 bins for the top bands)
+            float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+            const float* wq = mel.w + wo2;
+            const float* pq = P + st;
+            int i = 0;
+            for (; i + 4 <= n; i += 4) {
+              acc += wq[i] * pq[i];
+              a1 += wq[i + 1] * pq[i + 1];
+              a2 += wq[i + 2] * pq[i + 2];
+              a3 += wq[i + 3] * pq[i + 3];
+            }
+            for (; i < n; ++i) acc += wq[i] * pq[i];
+            acc = (acc + a1) + (a2 + a3);
           }
           res[q] = acc;
         }

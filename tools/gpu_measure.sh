@@ -112,6 +112,12 @@ for what in "$@"; do
         MST_GL_TABS=$v timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline \
           >> "$OUT/ab_gltab.jsonl" 2>> "$OUT/ab_gltab.err"
       done ;;
+    abmel)
+      for lib in "" variants/mel_head/libmst_hip.so "" variants/mel_head/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_mel.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload frontend --no-cpu-baseline \
+          >> "$OUT/ab_mel.jsonl" 2>> "$OUT/ab_mel.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
