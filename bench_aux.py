@@ -117,15 +117,17 @@ def _gl_traffic(n_iter):
         d = json.load(open(tj))
         per = {}
         for k, v in d.get("per_kernel", {}).items():
-            for key in ("gl_synth_kernel", "gl_seam_kernel", "stft_kernel<3>", "transpose_mag_kernel",
-                        "fillBufferAligned"):
+            # the complex STFT: stft_fm_kernel<3, ...> (late round 2) or stft_kernel<3> (before)
+            for key, name in (("gl_synth_kernel", "synth"), ("gl_seam_kernel", "seam"), ("stft_kernel<3>", "cx"),
+                              ("stft_fm_kernel<3,", "cx"), ("transpose_mag_kernel", "tmag"),
+                              ("fillBufferAligned", "memset")):
                 if key in k:
-                    per[key] = 2 * v["fetch_raw_per_launch"] + v["write_per_launch"]
-        if "gl_synth_kernel" not in per or "stft_kernel<3>" not in per:
+                    per[name] = 2 * v["fetch_raw_per_launch"] + v["write_per_launch"]
+        if "synth" not in per or "cx" not in per:
             continue
-        tot = ((n_iter + 1) * (per["gl_synth_kernel"] + per.get("gl_seam_kernel", 0.0))
-               + n_iter * per["stft_kernel<3>"] + per.get("transpose_mag_kernel", 0.0)
-               + per.get("fillBufferAligned", 0.0))  # the seam-zeroing memset (atomic-seam builds)
+        tot = ((n_iter + 1) * (per["synth"] + per.get("seam", 0.0))
+               + n_iter * per["cx"] + per.get("tmag", 0.0)
+               + per.get("memset", 0.0))  # the seam-zeroing memset (atomic-seam builds)
         return round(tot), f"profiles/{r}/gl_traffic.json ({d.get('build', '')})"
     return None, None
 
@@ -258,7 +260,7 @@ def griffinlim(args, world, rank, dev):
                   {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
                    "L": L, "n_fft": 2048, "hop": bench.HOP},
                   _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
-                        "gl_synth_kernel (atomic seams) + stft_kernel<COMPLEX> per iteration",
+                        "gl_synth_kernel (atomic seams) + stft_fm_kernel<COMPLEX> per iteration",
                         B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, {"kernel_ms": round(kms, 3)})]
 
 
