@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "mss_args.h"
 
 namespace {
 
@@ -1684,7 +1685,208 @@ int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, flo
   return MST_OK;
 }
 
+
+// ---------------------------------------------------------------------------
+// Multi-scale spectral loss, n = 1024 (mss.hip has the other sizes and the plan): the same
+// ownership, frame pairing and overlap-add as mss_wave_kernel, but each frame's transform is
+// fft1024_v2 in registers (z = w (p + i q) at n = lane + 64 j; permlane exchanges and one LDS
+// transpose, twiddles from the LDS tables) instead of five in-place LDS radix-4 stages. The
+// bins f and 1024 - f that P_f = (Z_f + conj Z_{n-f}) / 2 pairs sit in lanes l and 64 - l
+// (registers j and 15 - j), exchanged with ds_bpermute; the inverse transform of the packed
+// gradient spectra C is conj(fft1024_v2(conj C)), and C's upper half is routed back the same
+// way. The result goes to the wave's LDS buffer for the workgroup's ordered overlap-add.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int mss_reflect(int i, int L) {
+  i = i < 0 ? -i : i;
+  return i >= L ? 2 * (L - 1) - i : i;
+}
+
+__global__ __launch_bounds__(256, 3) void mss_fft1024_kernel(const MssArgs a) {
+  constexpr int N = 1024, H = N / 4, HALF = N / 2, W = 4, OWN = MSS_RWIN / 256;
+  __shared__ __attribute__((aligned(16))) c2 buf[W * SCR];  // per wave: FFT scratch, then G
+  __shared__ __attribute__((aligned(16))) FftTabs tb;
+  __shared__ float hw[N];
+  __shared__ float red[2][W];
+  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = (int)a.L;
+  const float* p = a.pred + (long long)b * a.L;
+  const float* q = a.target + (long long)b * a.L;
+  const bool grad = a.dpred != nullptr;
+  {
+    const float4* src = reinterpret_cast<const float4*>(&kFftTabs);
+    float4* dst = reinterpret_cast<float4*>(&tb);
+    for (int i = tid; i < TAB_F4; i += 256) dst[i] = src[i];
+    // periodic Hann 0.5 - 0.5 cos(2 pi n / 1024) = sin^2(pi n / 1024) = Im(W2048^n)^2
+    for (int n = tid; n < N; n += 256) {
+      const float2 e = kFftTabs.p[n & 511];
+      const float s = (n < 512) ? e.y : e.x;  // W2048^(512 + r) = -i W2048^r
+      hw[n] = s * s;
+    }
+  }
+  __syncthreads();
+  const int own_lo = w * MSS_RWIN;
+  const int f_own0 = w * (MSS_RWIN / H), f_own1 = min(f_own0 + MSS_RWIN / H, a.T);
+  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
+  c2* S = buf + wave * SCR;
+  float acc[OWN];
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
+  float s_abs = 0.f, s_log = 0.f;
+
+#pragma unroll 1
+  for (int t_round = f_lo; t_round < f_own1; t_round += 2 * W) {
+    const int t_base = t_round + 2 * wave;  // this wave's frame pair
+    if (t_base < f_own1) {                  // wave-uniform
+      int tid2 = tid;
+      __asm__ volatile("" : "+v"(tid2));
+      const int lane = tid2 & 63;
+      const int src = ((64 - lane) & 63) * 4;  // bperm partner: lane 64 - l
+      c2 zga[9], zgb[9];                      // gradient spectra at f = l + 64 j (j < 8), 512
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int t = t_base + pass;
+        const bool valid = t < f_own1;
+        c2 v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int n = lane + 64 * j;
+          v[j] = mk(0.f, 0.f);
+          if (valid) {
+            const int sidx = mss_reflect(t * H + n - HALF, L);
+            v[j] = mk(hw[n] * p[sidx], hw[n] * q[sidx]);
+          }
+        }
+        fft1024_v2(v, S, tb, lane);  // v[j] = Z[l + 64 j]
+        c2 zg[9];
+        c2 prev = v[0];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          c2 zf, zr;
+          if (j < 8) {
+            const c2 bpj = mk(bperm(src, v[15 - j].x), bperm(src, v[15 - j].y));
+            zr = lane == 0 ? prev : bpj;  // lane 0: Z[1024 - 64 j] is its own register 16 - j
+            prev = bpj;
+            zf = v[j];
+          } else {
+            zf = zr = v[8];  // f = 512 (meaningful in lane 0)
+          }
+          if (j < 8 && lane == 0 && j > 0) zr = v[16 - j];
+          const c2 P = (zf + conj(zr)) * 0.5f;
+          const c2 D = zf - conj(zr);
+          const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
+          const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
+          const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
+          const float lp = __log2f(sp + a.eps) * 0.69314718055994531f;
+          const float lt = __log2f(st + a.eps) * 0.69314718055994531f;
+          const bool bin = j < 8 || lane == 0;  // f = 512 only once
+          c2 g2 = mk(0.f, 0.f);
+          if (valid && bin) {
+            if (t >= f_own0) {
+              s_abs += fabsf(sp - st);
+              s_log += fabsf(lp - lt);
+            }
+            if (grad && sp > 0.f) {
+              const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
+              const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
+              g2 = P * (g * __builtin_amdgcn_rcpf(sp));
+            }
+          }
+          zg[j] = g2;
+        }
+#pragma unroll
+        for (int j = 0; j < 9; ++j) {
+          if (pass == 0) zga[j] = zg[j];
+          else zgb[j] = zg[j];
+        }
+      }
+      if (grad) {
+        // C = H^a + i H^b: c[f] into register j, c[1024 - f] to lane 64 - l, register 15 - j
+        c2 v[16];
+        c2 cn[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const c2 za = zga[j], zb = zgb[j];
+          const bool dc = lane == 0 && j == 0;  // f = 0: real parts only
+          v[j] = dc ? mk(za.x, zb.x) : mk(0.5f * (za.x - zb.y), 0.5f * (za.y + zb.x));
+          cn[j] = mk(0.5f * (za.x + zb.y), 0.5f * (-za.y + zb.x));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const c2 r = mk(bperm(src, cn[j].x), bperm(src, cn[j].y));
+          v[15 - j] = r;
+        }
+        if (lane == 0) {  // lane 0 holds c[64 r] for every r: c[512], and c[1024 - 64 j] from itself
+          v[8] = mk(zga[8].x, zgb[8].x);
+#pragma unroll
+          for (int j = 1; j < 8; ++j) v[16 - j] = cn[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = conj(v[j]);
+        fft1024_v2(v, S, tb, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the FFT's transpose reads of S are done
+#pragma unroll
+        for (int j = 0; j < 16; ++j) S[lane + 64 * j] = conj(v[j]);  // G[n]: frame a in x, b in y
+      }
+    }
+    if (!grad) continue;
+    __syncthreads();
+    const int r_hi = min(t_round + 2 * W, f_own1);
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const int sp = own_lo + tid + 256 * i;
+      const int th = sp / H;
+      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
+      float vv = acc[i];
+      for (int t = t0; t <= t1; ++t) {
+        const int j = sp - t * H;
+        const int rel = t - t_round, ww = rel >> 1;
+        const c2 g = buf[ww * SCR + j];
+        vv += hw[j] * ((rel & 1) ? g.y : g.x);
+      }
+      acc[i] = vv;
+    }
+    __syncthreads();
+  }
+
+  s_abs = wave_sum(s_abs);
+  s_log = wave_sum(s_log);
+  if ((tid & 63) == 0) {
+    red[0][wave] = s_abs;
+    red[1][wave] = s_log;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float sa = 0.f, sl = 0.f;
+    for (int i = 0; i < W; ++i) {
+      sa += red[0][i];
+      sl += red[1][i];
+    }
+    a.partial[((long long)b * a.nwg + w) * 2] = sa;
+    a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
+  }
+  if (!grad) return;
+  float* dp = a.dpred + (long long)b * a.L;
+  float* ed = a.edges + (long long)b * N;
+  const int own_hi = min(own_lo + MSS_RWIN, L + N);
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const int pp = own_lo + tid + 256 * i;
+    if (pp >= own_hi) continue;
+    const float vv = acc[i];
+    const int x = pp - HALF;
+    if (x < 0) ed[pp] = vv;
+    else if (x >= L) ed[HALF + (x - L)] = vv;
+    else dp[x] = a.accumulate ? dp[x] + vv : vv;
+  }
+}
+
 }  // namespace
+
+void mss_fft1024_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st) {
+  hipLaunchKernelGGL(mss_fft1024_kernel, dim3(nwg, B), dim3(256), 0, st, a);
+}
 
 extern "C" {
 

@@ -20,10 +20,11 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "mss_args.h"
 
 namespace {
 
-constexpr int RWIN = 4096;   // padded samples owned per workgroup
+constexpr int RWIN = MSS_RWIN;  // padded samples owned per workgroup
 constexpr int CAP = 2048;    // complex values per LDS FFT buffer
 #ifndef MSS_NT
 #define MSS_NT 256
@@ -130,17 +131,6 @@ __device__ __forceinline__ int reflect(int i, int L) {
   return i >= L ? 2 * (L - 1) - i : i;
 }
 
-struct MssArgs {
-  const float* pred;
-  const float* target;
-  long long L;
-  int T, nwg;
-  float alpha, eps, inv_cnt;
-  float* dpred;        // (B, L) or null
-  int accumulate;      // add into dpred (sizes after the first)
-  float* edges;        // (B, n): gradient of the reflect-pad samples, head n/2 then tail n/2
-  float* partial;      // (B, nwg, 2): per-workgroup sums of |dS| and |dlogS|
-};
 
 template <int LOG2N>
 __global__ __launch_bounds__(NT) void mss_scale_kernel(const MssArgs a) {
@@ -619,6 +609,15 @@ bool mss_legacy() {
   return v;
 }
 
+// MST_MSS_REG=0: n = 1024 on mss_wave_kernel instead of the register-resident FFT (A/B)
+bool mss_reg() {
+  static const bool v = [] {
+    const char* e = getenv("MST_MSS_REG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int log2i(int n) {
   int l = 0;
   while ((1 << l) < n) ++l;
@@ -702,7 +701,10 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
         case 7: mss_wave_kernel<7><<<grid, 256, 0, st>>>(a); break;
         case 8: mss_wave_kernel<8><<<grid, 256, 0, st>>>(a); break;
         case 9: mss_wave_kernel<9><<<grid, 256, 0, st>>>(a); break;
-        case 10: mss_wave_kernel<10><<<grid, 256, 0, st>>>(a); break;
+        case 10:
+          if (mss_reg()) mss_fft1024_launch(a, grid.x, grid.y, st);
+          else mss_wave_kernel<10><<<grid, 256, 0, st>>>(a);
+          break;
         default: mss_wave_kernel<11><<<grid, 256, 0, st>>>(a); break;
       }
     }

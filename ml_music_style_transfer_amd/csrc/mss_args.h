@@ -1,0 +1,21 @@
+// Arguments of the multi-scale spectral loss kernels (mss.hip), shared with the n = 1024 kernel in
+// fft.hip, which reuses fft.hip's register-resident 1024-point FFT.
+#pragma once
+#include <hip/hip_runtime.h>
+
+constexpr int MSS_RWIN = 4096;  // padded samples owned per workgroup
+
+struct MssArgs {
+  const float* pred;
+  const float* target;
+  long long L;
+  int T, nwg;
+  float alpha, eps, inv_cnt;
+  float* dpred;        // (B, L) or null
+  int accumulate;      // add into dpred (sizes after the first)
+  float* edges;        // (B, n): gradient of the reflect-pad samples, head n/2 then tail n/2
+  float* partial;      // (B, nwg, 2): per-workgroup sums of |dS| and |dlogS|
+};
+
+// n = 1024: grid (nwg, B), 256 threads (fft.hip)
+void mss_fft1024_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st);
