@@ -1882,10 +1882,224 @@ __global__ __launch_bounds__(256, 3) void mss_fft1024_kernel(const MssArgs a) {
   }
 }
 
+
+// n = 2048: a 2048-point transform as one radix-2 step plus two fft1024_v2 (even and odd output
+// bins, z at n = lane + 64 j, j < 32, 32 complex per lane). Forward (decimation in frequency):
+// E = FFT1024(z[n] + z[n + 1024]) = X[2k], O = FFT1024((z[n] - z[n + 1024]) W2048^n) = X[2k + 1].
+// The partner of X[2k] is X[2048 - 2k] = E[1024 - k] (lane 64 - l, register 15 - j) and of
+// X[2k + 1] is X[2047 - 2k] = O[1023 - k] (lane 63 - l, register 15 - j). The inverse runs the
+// other way (decimation in time): g = IFFT1024(c_even) + W2048^-n IFFT1024(c_odd), so the packed
+// gradient spectra are built directly in the even / odd layouts. The window comes from the
+// twiddle table (0.5 - 0.5 Re W2048^n), keeping LDS at 76 KB (two workgroups per CU).
+__device__ __forceinline__ c2 w2048(const FftTabs& tb, int n) {  // W2048^n, 0 <= n < 1024
+  const float2 e = tb.p[n & 511];
+  return n < 512 ? mk(e.x, e.y) : mk(e.y, -e.x);  // W^(512 + r) = -i W^r
+}
+
+// loss terms and gradient spectrum of one bin from Z_f (zf) and Z_(n-f) (zr)
+__device__ __forceinline__ c2 mss_bin(c2 zf, c2 zr, bool use, bool own, bool grad, const MssArgs& a,
+                                      float& s_abs, float& s_log) {
+  const c2 P = (zf + conj(zr)) * 0.5f;
+  const c2 D = zf - conj(zr);
+  const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
+  const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
+  const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
+  c2 g2 = mk(0.f, 0.f);
+  if (use) {
+    if (own) {
+      s_abs += fabsf(sp - st);
+      s_log += fabsf(__log2f(sp + a.eps) * 0.69314718055994531f - __log2f(st + a.eps) * 0.69314718055994531f);
+    }
+    if (grad && sp > 0.f) {
+      const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
+      const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
+      g2 = P * (g * __builtin_amdgcn_rcpf(sp));
+    }
+  }
+  return g2;
+}
+
+__global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
+  constexpr int N = 2048, H = N / 4, HALF = N / 2, W = 4, OWN = MSS_RWIN / 256;
+  __shared__ __attribute__((aligned(16))) c2 buf[W * N];  // per wave: FFT scratch, then G
+  __shared__ __attribute__((aligned(16))) FftTabs tb;
+  __shared__ float red[2][W];
+  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int L = (int)a.L;
+  const float* p = a.pred + (long long)b * a.L;
+  const float* q = a.target + (long long)b * a.L;
+  const bool grad = a.dpred != nullptr;
+  {
+    const float4* src = reinterpret_cast<const float4*>(&kFftTabs);
+    float4* dst = reinterpret_cast<float4*>(&tb);
+    for (int i = tid; i < TAB_F4; i += 256) dst[i] = src[i];
+  }
+  __syncthreads();
+  auto hann = [&](int n) {  // periodic Hann 0.5 - 0.5 cos(2 pi n / 2048) = 0.5 - 0.5 Re W2048^n
+    const float2 e = tb.p[n & 511];
+    const int qd = (n >> 9) & 3;  // W^(512 qd + r) = (-i)^qd W^r
+    const float re = qd == 0 ? e.x : (qd == 1 ? e.y : (qd == 2 ? -e.x : -e.y));
+    return 0.5f - 0.5f * re;
+  };
+  const int own_lo = w * MSS_RWIN;
+  const int f_own0 = w * (MSS_RWIN / H), f_own1 = min(f_own0 + MSS_RWIN / H, a.T);
+  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
+  c2* S = buf + wave * N;
+  float acc[OWN];
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
+  float s_abs = 0.f, s_log = 0.f;
+
+#pragma unroll 1
+  for (int t_round = f_lo; t_round < f_own1; t_round += 2 * W) {
+    const int t_base = t_round + 2 * wave;
+    if (t_base < f_own1) {  // wave-uniform
+      int tid2 = tid;
+      __asm__ volatile("" : "+v"(tid2));
+      const int lane = tid2 & 63;
+      const int src_e = ((64 - lane) & 63) * 4, src_o = (63 - lane) * 4;
+      c2 zae[9], zao[8], zbe[9], zbo[8];  // gradient spectra: even bins 2k (k = l + 64 j, 512), odd 2k + 1
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int t = t_base + pass;
+        const bool valid = t < f_own1;
+        c2 ve[16], vo[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int n = lane + 64 * j;
+          c2 x0 = mk(0.f, 0.f), x1 = mk(0.f, 0.f);
+          if (valid) {
+            const int s0 = mss_reflect(t * H + n - HALF, L), s1 = mss_reflect(t * H + n + 1024 - HALF, L);
+            const float h0 = hann(n), h1 = hann(n + 1024);
+            x0 = mk(h0 * p[s0], h0 * q[s0]);
+            x1 = mk(h1 * p[s1], h1 * q[s1]);
+          }
+          ve[j] = x0 + x1;
+          vo[j] = cmul(x0 - x1, w2048(tb, n));
+        }
+        fft1024_v2(ve, S, tb, lane);  // ve[j] = X[2 (l + 64 j)]
+        fft1024_v2(vo, S, tb, lane);  // vo[j] = X[2 (l + 64 j) + 1]
+        const bool own = t >= f_own0;
+        c2 prev = ve[0];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // even bin f = 2k: partner E[1024 - k] (lane 64 - l, register 15 - j; lane 0: its own 16 - j)
+          const c2 bpe = mk(bperm(src_e, ve[15 - j].x), bperm(src_e, ve[15 - j].y));
+          const c2 zre = lane == 0 ? prev : bpe;
+          prev = bpe;
+          const c2 ge = mss_bin(ve[j], zre, valid, own, grad, a, s_abs, s_log);
+          // odd bin f = 2k + 1: partner O[1023 - k] (lane 63 - l, register 15 - j)
+          const c2 zro = mk(bperm(src_o, vo[15 - j].x), bperm(src_o, vo[15 - j].y));
+          const c2 go = mss_bin(vo[j], zro, valid, own, grad, a, s_abs, s_log);
+          if (pass == 0) { zae[j] = ge; zao[j] = go; } else { zbe[j] = ge; zbo[j] = go; }
+        }
+        // f = 1024 = 2 x 512: E[512], its own partner (lane 0, register 8)
+        const c2 gn = mss_bin(ve[8], ve[8], valid && lane == 0, own, grad, a, s_abs, s_log);
+        if (pass == 0) zae[8] = gn; else zbe[8] = gn;
+      }
+      if (grad) {
+        // c_even[k] = C[2k], c_odd[k] = C[2k + 1], C = H^a + i H^b (H_f = Z_f / 2, H_(n-f) = conj)
+        c2 ce[16], co[16], cne[8], cno[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool dc = lane == 0 && j == 0;
+          ce[j] = dc ? mk(zae[j].x, zbe[j].x) : mk(0.5f * (zae[j].x - zbe[j].y), 0.5f * (zae[j].y + zbe[j].x));
+          cne[j] = mk(0.5f * (zae[j].x + zbe[j].y), 0.5f * (-zae[j].y + zbe[j].x));
+          co[j] = mk(0.5f * (zao[j].x - zbo[j].y), 0.5f * (zao[j].y + zbo[j].x));
+          cno[j] = mk(0.5f * (zao[j].x + zbo[j].y), 0.5f * (-zao[j].y + zbo[j].x));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          // C[2048 - 2k] = c_even[1024 - k]: to lane 64 - l, register 15 - j
+          ce[15 - j] = mk(bperm(src_e, cne[j].x), bperm(src_e, cne[j].y));
+          // C[2047 - 2k] = c_odd[1023 - k]: to lane 63 - l, register 15 - j
+          co[15 - j] = mk(bperm(src_o, cno[j].x), bperm(src_o, cno[j].y));
+        }
+        if (lane == 0) {  // c_even[512] = C[1024]; c_even[1024 - 64 j] from itself
+          ce[8] = mk(zae[8].x, zbe[8].x);
+#pragma unroll
+          for (int j = 1; j < 8; ++j) ce[16 - j] = cne[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          ce[j] = conj(ce[j]);
+          co[j] = conj(co[j]);
+        }
+        fft1024_v2(ce, S, tb, lane);  // conj(IFFT1024(c_even)) at n' = l + 64 j
+        fft1024_v2(co, S, tb, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int n = lane + 64 * j;
+          const c2 ge = conj(ce[j]);
+          const c2 go = cmul(conj(co[j]), conj(w2048(tb, n)));  // W2048^-n IFFT(c_odd)
+          S[n] = ge + go;
+          S[n + 1024] = ge - go;
+        }
+      }
+    }
+    if (!grad) continue;
+    __syncthreads();
+    const int r_hi = min(t_round + 2 * W, f_own1);
+#pragma unroll
+    for (int i = 0; i < OWN; ++i) {
+      const int sp = own_lo + tid + 256 * i;
+      const int th = sp / H;
+      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
+      float vv = acc[i];
+      for (int t = t0; t <= t1; ++t) {
+        const int j = sp - t * H;
+        const int rel = t - t_round, ww = rel >> 1;
+        const c2 g = buf[ww * N + j];
+        vv += hann(j) * ((rel & 1) ? g.y : g.x);
+      }
+      acc[i] = vv;
+    }
+    __syncthreads();
+  }
+
+  s_abs = wave_sum(s_abs);
+  s_log = wave_sum(s_log);
+  if ((tid & 63) == 0) {
+    red[0][wave] = s_abs;
+    red[1][wave] = s_log;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float sa = 0.f, sl = 0.f;
+    for (int i = 0; i < W; ++i) {
+      sa += red[0][i];
+      sl += red[1][i];
+    }
+    a.partial[((long long)b * a.nwg + w) * 2] = sa;
+    a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
+  }
+  if (!grad) return;
+  float* dp = a.dpred + (long long)b * a.L;
+  float* ed = a.edges + (long long)b * N;
+  const int own_hi = min(own_lo + MSS_RWIN, L + N);
+#pragma unroll
+  for (int i = 0; i < OWN; ++i) {
+    const int pp = own_lo + tid + 256 * i;
+    if (pp >= own_hi) continue;
+    const float vv = acc[i];
+    const int x = pp - HALF;
+    if (x < 0) ed[pp] = vv;
+    else if (x >= L) ed[HALF + (x - L)] = vv;
+    else dp[x] = a.accumulate ? dp[x] + vv : vv;
+  }
+}
+
 }  // namespace
 
 void mss_fft1024_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st) {
   hipLaunchKernelGGL(mss_fft1024_kernel, dim3(nwg, B), dim3(256), 0, st, a);
+}
+
+void mss_fft2048_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st) {
+  hipLaunchKernelGGL(mss_fft2048_kernel, dim3(nwg, B), dim3(256), 0, st, a);
 }
 
 extern "C" {

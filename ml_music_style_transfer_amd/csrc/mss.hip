@@ -705,7 +705,10 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
           if (mss_reg()) mss_fft1024_launch(a, grid.x, grid.y, st);
           else mss_wave_kernel<10><<<grid, 256, 0, st>>>(a);
           break;
-        default: mss_wave_kernel<11><<<grid, 256, 0, st>>>(a); break;
+        default:
+          if (mss_reg()) mss_fft2048_launch(a, grid.x, grid.y, st);
+          else mss_wave_kernel<11><<<grid, 256, 0, st>>>(a);
+          break;
       }
     }
     MST_CHECK_LAUNCH();
