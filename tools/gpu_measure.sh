@@ -126,6 +126,14 @@ for what in "$@"; do
         MST_MSS_REG=$v timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 \
           >> "$OUT/ab_mssreg.jsonl" 2>> "$OUT/ab_mssreg.err"
       done ;;
+    abmssil)
+      timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+        -k "multiscale or mss" > "$OUT/pytest_mssil.log" 2>&1
+      for v in 1 0 1 0; do
+        echo "== MST_MSS_IL=$v" >> "$OUT/ab_mssil.jsonl"
+        MST_MSS_IL=$v timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 \
+          >> "$OUT/ab_mssil.jsonl" 2>> "$OUT/ab_mssil.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
