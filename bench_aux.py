@@ -132,6 +132,21 @@ def _gl_traffic(n_iter):
     return None, None
 
 
+def _mss_traffic():
+    """HBM bytes of one multi-scale loss call (six size kernels + edge fold + loss reduce) from the
+    newest round's PMC passes over the loss leg (profiles/r*/mss_traffic.json)."""
+    pdir = os.path.join(ROOT, "profiles")
+    for r in sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) if os.path.isdir(pdir) else []:
+        tj = os.path.join(pdir, r, "mss_traffic.json")
+        if not os.path.exists(tj):
+            continue
+        d = json.load(open(tj))
+        tot = sum(2 * v["fetch_raw_per_launch"] + v["write_per_launch"]
+                  for k, v in d.get("per_kernel", {}).items() if "mss_" in k)
+        return round(tot), f"profiles/{r}/mss_traffic.json ({d.get('build', '')})"
+    return None, None
+
+
 def _roof(achieved_gbs, kernel, bytes_per_launch, traffic_key=None, traffic=None):
     if traffic is not None:
         traffic, src = traffic
@@ -299,8 +314,9 @@ def mss(args, world, rank, dev):
                   world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
                    "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
-                  _roof(B * bpp / (kms * 1e-3) / 1e9, "mss_scale_kernel<6..11> + fold + loss reduce",
-                        B * bpp), cpu,
+                  _roof(B * bpp / (kms * 1e-3) / 1e9,
+                        "mss_wave_kernel<6..9>, mss_fft1024/2048_kernel + fold + loss reduce",
+                        B * bpp, traffic=_mss_traffic()), cpu,
                   {"kernel_ms": round(kms, 4), "approx_fft_gflop_per_step": round(B * flops / 1e9, 2)})]
 
 

@@ -32,6 +32,11 @@ for what in "$@"; do
         python3 bench_aux.py --workload griffinlim --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcgl_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcgl_write" -o run -- \
         python3 bench_aux.py --workload griffinlim --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcgl_write.log" 2>&1 ;;
+    pmcmss)
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcmss_fetch" -o run -- \
+        python3 bench_aux.py --workload mss --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcmss_fetch.log" 2>&1
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcmss_write" -o run -- \
+        python3 bench_aux.py --workload mss --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcmss_write.log" 2>&1 ;;
     aux)
       timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
     layers)
