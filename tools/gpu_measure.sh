@@ -139,6 +139,14 @@ for what in "$@"; do
         MST_MSS_IL=$v timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 \
           >> "$OUT/ab_mssil.jsonl" 2>> "$OUT/ab_mssil.err"
       done ;;
+    abbr)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -v --timeout 120 \
+        --timeout-method thread > "$OUT/pytest_br.log" 2>&1
+      for lib in "" variants/br_head/libmst_hip.so "" variants/br_head/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_br.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_br.jsonl" 2>> "$OUT/ab_br.err"
+      done ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
