@@ -147,13 +147,13 @@ def aux_legs(world, rank, dev, cpu):
     training step (bench_aux.py's legs, shortened; one-thread oracle CPU baselines)."""
     import bench_aux
     a = argparse.Namespace(steps=10, warmup=2, clips=256, pairs=32, no_cpu_baseline=not cpu,
-                           parallel_cpu=False)
+                           parallel_cpu=False, no_parity=False)
     out = {}
     for fn in (bench_aux.frontend, bench_aux.griffinlim, bench_aux.mss):
         for ln in fn(a, world, rank, dev):
             key = ln["config"]["workload"]
             out[key] = {k: ln[k] for k in ("metric", "value", "unit", "ms_per_step", "kernel_ms",
-                                           "roofline", "cpu_baseline") if k in ln}
+                                           "roofline", "cpu_baseline", "parity") if k in ln}
     return out
 
 

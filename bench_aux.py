@@ -205,6 +205,31 @@ def _cpu_parallel_rate(name, clips):
             "sample": f"{len(clips)} clips, multiprocessing pool of {procs} spawned workers"}
 
 
+def _sampled(B):
+    """Clips checked against the oracle after the timed region: one per residue mod 8 (the
+    persistent STFT kernel's XCD groups) and the last clip."""
+    return sorted({min(B - 1, 9 * r) for r in range(8)} | {B - 1})
+
+
+def _frontend_parity(name, out, x):
+    """Sampled clips of the measured output vs oracle/spectral_ref (tolerances of
+    tests/test_gpu_config2.py: log-power 1e-4 absolute, mel 1e-4 of the frame's peak)."""
+    from oracle import spectral_ref as SR
+    worst = 0.0
+    idx = _sampled(len(x))
+    for b in idx:
+        if name == "logpow":
+            err = float(np.abs(out[b] - SR.logpow(x[b], 2048, bench.HOP)).max())
+            tol = 1e-4
+        else:
+            ref = SR.melspec(x[b], bench.SR, 2048, bench.HOP)
+            err = float((np.abs(out[b] - ref) / (ref.max(axis=0, keepdims=True) + 1e-12)).max())
+            tol = 1e-4
+        worst = max(worst, err)
+    assert worst <= tol, f"{name}: sampled clips differ from the oracle by {worst} > {tol}"
+    return {"clips": idx, "max_err": worst, "tol": tol, "ok": True}
+
+
 def frontend(args, world, rank, dev):
     from ml_music_style_transfer_amd import spectral
     from oracle import spectral_ref as SR
@@ -235,14 +260,33 @@ def frontend(args, world, rank, dev):
                     cpu["parallel"] = _cpu_parallel_rate(name, list(x[:min(B, 256)]))
                 except Exception as e:  # a baseline leg must not cost the measured line
                     cpu["parallel"] = {"error": repr(e)[:200]}
+        extra = {"kernel_ms": round(kms, 4)}
+        if rank == 0 and not args.no_parity:
+            extra["parity"] = _frontend_parity(name, fn().cpu().numpy(), x)
         res.append(_line(f"STFT {name} clips/s, 256 x 4 s @ 16 kHz", world * B / dt, "clips/s", world,
                          args.steps, args.warmup, dt * 1e3,
                          {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,
                           "n_fft": 2048, "hop": bench.HOP},
                          _roof(B * bpc / (kms * 1e-3) / 1e9, kern, B * bpc,
-                               tkey if B == 256 else None), cpu,
-                         {"kernel_ms": round(kms, 4)}))
+                               tkey if B == 256 else None), cpu, extra))
     return res
+
+
+def _gl_parity(S, y, idx, n_iter):
+    """Spectral convergence of sampled clips of the measured output vs the oracle's Griffin-Lim
+    from the same (all-ones) init: within 2 % (tests/test_gpu_config2.py's bound)."""
+    from ml_music_style_transfer_amd import spectral
+    from oracle import spectral_ref as SR
+    rows = []
+    for b in idx:
+        Sb = S[b].cpu().double().numpy()
+        sc = spectral.spectral_convergence(S[b:b + 1], y[b:b + 1], hop=bench.HOP)
+        yr = SR.griffinlim(Sb, n_iter=n_iter, hop=bench.HOP)
+        sc_ref = float(np.linalg.norm(np.abs(SR.stft(yr, 2048, bench.HOP, out_dtype=None)) - Sb)
+                       / np.linalg.norm(Sb))
+        assert sc <= sc_ref * 1.02 + 1e-4, f"Griffin-Lim clip {b}: convergence {sc} vs oracle {sc_ref}"
+        rows.append({"clip": b, "spectral_convergence": round(sc, 6), "oracle": round(sc_ref, 6)})
+    return {"clips": rows, "tol": "sc <= 1.02 sc_oracle + 1e-4", "ok": True}
 
 
 def griffinlim(args, world, rank, dev):
@@ -270,13 +314,16 @@ def griffinlim(args, world, rank, dev):
         cpu = {"value": round(1.0 / (c * n_iter), 3), "unit": "clips/s (60 iterations)", "cores": 1,
                "kind": "port", "sample": "1 clip x 10 iterations of oracle/spectral_ref.griffinlim "
                                          "(NumPy float64, 1 thread), scaled to 60 iterations"}
+    extra = {"kernel_ms": round(kms, 3)}
+    if rank == 0 and not args.no_parity:
+        extra["parity"] = _gl_parity(S, fn(), [0, B - 1], n_iter)
     return [_line("Griffin-Lim clips/s (60 iterations), 256 x 4 s @ 16 kHz", world * B / dt,
                   "clips/s", world, steps, 1, dt * 1e3,
                   {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
                    "L": L, "n_fft": 2048, "hop": bench.HOP},
                   _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
                         "gl_synth_kernel (atomic seams) + stft_fm_kernel<COMPLEX> per iteration",
-                        B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, {"kernel_ms": round(kms, 3)})]
+                        B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, extra)]
 
 
 def mss(args, world, rank, dev):
@@ -310,14 +357,23 @@ def mss(args, world, rank, dev):
         cpu = {"value": round(1.0 / c, 3), "unit": "clip-pairs/s", "cores": 1, "kind": "port",
                "sample": "1 clip pair (10 s @ 22.05 kHz), loss + gradient by "
                          "oracle/spectral_ref.multiscale_spectral_loss_grad (NumPy float64)"}
+    extra = {"kernel_ms": round(kms, 4), "approx_fft_gflop_per_step": round(B * flops / 1e9, 2)}
+    if rank == 0 and not args.no_parity:
+        p0 = pred.detach()[:1].clone().requires_grad_(True)
+        l0 = spectral.multiscale_spectral_loss(p0, tgt[:1], sizes=sizes)
+        ref, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
+                                                  tgt[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
+        rel = abs(l0.item() - ref) / abs(ref)
+        assert rel <= 1e-4, f"multi-scale loss of pair 0: {l0.item()} vs oracle {ref}"
+        extra["parity"] = {"pair": 0, "loss": l0.item(), "oracle": ref, "rel_err": rel,
+                           "tol": 1e-4, "ok": True}
     return [_line("multi-scale spectral loss fwd+grad clip-pairs/s, 10 s @ 22.05 kHz, 6 FFT sizes",
                   world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
                    "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
                   _roof(B * bpp / (kms * 1e-3) / 1e9,
                         "mss_wave_kernel<6..9>, mss_fft1024/2048_kernel + fold + loss reduce",
-                        B * bpp, traffic=_mss_traffic()), cpu,
-                  {"kernel_ms": round(kms, 4), "approx_fft_gflop_per_step": round(B * flops / 1e9, 2)})]
+                        B * bpp, traffic=_mss_traffic()), cpu, extra)]
 
 
 def main():
@@ -328,6 +384,8 @@ def main():
     ap.add_argument("--clips", type=int, default=256)
     ap.add_argument("--pairs", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the sampled-clip oracle check after the timed region")
     args = ap.parse_args()
     world, rank, dev = _dist()
     from ml_music_style_transfer_amd import _lib

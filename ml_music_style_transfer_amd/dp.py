@@ -36,7 +36,7 @@ def allreduce_gradients(model, bucket_bytes=DEFAULT_BUCKET_BYTES, async_op=False
     world = dist.get_world_size()
     per = max(1, bucket_bytes // 4)
     works = []
-    op = dist.ReduceOp.AVG if dist.get_backend() == "nccl" else dist.ReduceOp.SUM
+    op = dist.ReduceOp.AVG if native_avg() else dist.ReduceOp.SUM
     for s in range(0, n, per):
         w = dist.all_reduce(grad[s:min(n, s + per)], op=op, async_op=async_op)
         if async_op:

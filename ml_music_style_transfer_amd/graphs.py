@@ -83,6 +83,7 @@ class GraphedTrainStep:
         self.warmup = warmup
         self.calls = 0
         self.graph = None
+        self._captured_st = None  # the flat Adam state whose m/v buffers the graph names
         self.inputs = None
         g = optimizer.param_groups[0]
         self.b1, self.b2 = g["betas"]
@@ -107,6 +108,10 @@ class GraphedTrainStep:
         elif st["step"] != self._host_step:  # eager optimizer steps ran in between
             self.step_dev.fill_(float(st["step"]))
         self._host_step = st["step"]
+        if self.graph is not None and st is not self._captured_st:
+            # the optimizer rebuilt its flat moments (load_state_dict): the captured graph
+            # still names the old m/v buffers, so capture again over the new ones
+            self.graph = None
         return st
 
     def _program(self, st):
@@ -147,6 +152,7 @@ class GraphedTrainStep:
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph):
                 self._program(st)
+            self._captured_st = st
             self.graph.replay()
         self.calls += 1
         self.opt._count_step(st, self.params)

@@ -70,12 +70,15 @@ def _dst(spec):
 
 
 # Workspace arena: one grow-only scratch buffer per (device, launch stream). Launches on one
-# stream are ordered, so consecutive GEMM / loss / Griffin-Lim launches share it instead of
-# paying an allocator round trip each. A buffer that is outgrown is retired, never freed: a
-# captured hipGraph may still name it. Under stream capture the arena is bypassed and each
-# launch takes a fresh buffer from the graph's private pool (torch's capture semantics).
+# stream are ordered, so consecutive GEMM split-K slabs and loss partials share it instead of
+# paying an allocator round trip each. An outgrown buffer is simply dropped: torch's caching
+# allocator hands its block out again only in this stream's order, after the launches already
+# queued on it. Under stream capture the arena is bypassed (each launch takes a fresh buffer
+# from the graph's private pool, torch's capture semantics), so no graph names an arena
+# buffer. Requests above ARENA_MAX_BYTES (Griffin-Lim's multi-GB clip chunks) are one-off
+# allocations that return to the allocator after the call instead of staying pinned here.
 _ARENA = {}
-_RETIRED = []
+ARENA_MAX_BYTES = 256 << 20
 
 
 def workspace(nbytes, device):
@@ -83,14 +86,14 @@ def workspace(nbytes, device):
     if nbytes == 0:
         return None, 0
     n = (nbytes + 3) // 4
-    if torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_current_stream_capturing() or nbytes > ARENA_MAX_BYTES:
         return torch.empty(n, device=device, dtype=torch.float32), 4 * n
     key = (device.index, L.stream().value)
     buf = _ARENA.get(key)
     if buf is None or buf.numel() < n:
         if buf is not None:
-            _RETIRED.append(buf)
-            n = max(n, 2 * buf.numel())
+            n = min(max(n, 2 * buf.numel()), ARENA_MAX_BYTES // 4)
+        _ARENA[key] = None  # release the outgrown block before taking the larger one
         buf = _ARENA[key] = torch.empty(n, device=device, dtype=torch.float32)
     return buf, 4 * buf.numel()
 

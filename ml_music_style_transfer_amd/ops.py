@@ -218,6 +218,10 @@ def _mss_setup(ctx, inputs, output):
 def _mss_backward(ctx, g_loss, g_d):
     (d,) = ctx.saved_tensors
     if d.numel() == 0:
+        if ctx.needs_input_grad[0]:
+            raise RuntimeError("mst::mss_loss was called with with_grad=False on a pred that "
+                               "requires grad: call it with with_grad=True (or use "
+                               "spectral.multiscale_spectral_loss, which chooses the flag)")
         return None, None, None, None, None, None
     return d * g_loss, None, None, None, None, None
 

@@ -10,6 +10,8 @@ restated in midi.py / wavio.py, HDF5 written through h5.py.
 """
 import glob
 
+import os
+
 import numpy as np
 import torch
 
@@ -223,16 +225,32 @@ def get_data(data_dir, dataset_outpath, data_type, debug=False, h=hp):
     return h5name
 
 
+def resolve_data_dir(data_dir, extract_to=None):
+    """preprocess.py:204-210: a zip `-data-dir` is unpacked into the working directory (or
+    `extract_to`) and replaced by the directory of its first member; a directory is returned
+    as is."""
+    import zipfile
+    if not zipfile.is_zipfile(data_dir):
+        return data_dir
+    print("Extracting zip file to local")
+    dest = os.getcwd() if extract_to is None else extract_to
+    with zipfile.ZipFile(data_dir) as zf:
+        first = zf.namelist()[0]
+        zf.extractall(dest)
+    return os.path.join(dest, os.path.dirname(first))
+
+
 def main(args):
-    """preprocess.py:203-215 without its zip extraction (out of scope): `-data-dir`
-    is an already-extracted directory."""
-    return get_data(args.data_dir, args.dataset_outpath, args.data_type, args.debug)
+    """preprocess.py:203-215: optional zip extraction, then get_data."""
+    data_dir = resolve_data_dir(args.data_dir)
+    return get_data(data_dir, args.dataset_outpath, args.data_type, args.debug)
 
 
 def parse_args(argv=None):
     import argparse
     parser = argparse.ArgumentParser()
-    parser.add_argument("-data-dir", type=str, required=True)
+    parser.add_argument("-data-dir", type=str, required=True,
+                        help="dataset directory, or a zip file that is extracted first")
     parser.add_argument("-dataset-outpath", type=str, required=True)
     parser.add_argument("-max-chunks-per-song", type=int, default=100)
     parser.add_argument("-data-type", type=str, default='train', choices=['train', 'test'])

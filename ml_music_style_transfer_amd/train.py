@@ -131,9 +131,8 @@ class Adam(torch.optim.Optimizer):
 
     def _count_step(self, st, params):
         st["step"] += 1
-        step_t = torch.tensor(float(st["step"]))
-        for p in params:
-            self.state[p]["step"] = step_t
+        for p in params:  # one tensor per parameter: the per-parameter path adds in place
+            self.state[p]["step"] = torch.tensor(float(st["step"]))
 
     @torch.no_grad()
     def step(self, closure=None):

@@ -148,3 +148,51 @@ def test_overlapped_bucket_allreduce_gloo():
         assert nb > 2
         assert launched == sorted(launched) and launched[0] >= 1  # issued during "backward"
         torch.testing.assert_close(g, mean, rtol=1e-6, atol=1e-6)
+
+
+def _native_avg_worker(rank, world, port, sizes, bucket, q):
+    """The RCCL-only branches (dp.native_avg() True: ReduceOp.AVG issued, no SUM-then-scale in
+    wait_bucket / allreduce_gradients) over gloo through tests/_rccl_emulation.py."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import _rccl_emulation
+    dp = _rccl_emulation.install()
+    m = _LayeredModel(sizes, rank)
+    r = dp.OverlappedAllReduce(m, bucket_bytes=bucket)
+    r.begin()
+    for i in range(0, len(m.params), 2):
+        r.ready(m.params[i:i + 2])
+    native = all(r.scaled)          # every issued bucket took the AVG branch
+    r.finish()
+    over = m.gradbuf.clone()
+    m2 = _LayeredModel(sizes, rank)
+    dp.wait_all(dp.allreduce_gradients(m2, bucket_bytes=bucket, async_op=True))
+    q.put((rank, native, over, m2.gradbuf.clone()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_avg_branches_emulated_gloo():
+    """OverlappedAllReduce._launch / wait_bucket and allreduce_gradients on the path RCCL takes
+    (ReduceOp.AVG, no host-side scale): equal to the rank mean, and bitwise equal between the
+    overlapped and the post-backward forms."""
+    sizes = [5, 17, 3, 64, 9, 1, 33, 8]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_avg_worker, args=(r, world, port, sizes, 4 * 24, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mean = sum(_LayeredModel(sizes, r).gradbuf for r in range(world)) / world
+    for r in range(world):
+        native, over, post = res[r]
+        assert native
+        torch.testing.assert_close(over, mean, rtol=1e-6, atol=1e-6)
+        assert torch.equal(over, post)

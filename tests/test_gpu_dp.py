@@ -158,8 +158,10 @@ def test_train_main_data_parallel_two_ranks(cuda, tmp_path, monkeypatch):
     assert (exp / ("checkpoint-%d.tar" % res[0][2])).exists() and (exp / "hyperparams.json").exists()
 
 
-def _variants_worker(rank, world, port, q):
-    """Three data-parallel update paths on the same two steps, and gradient accumulation."""
+def _variants_worker(rank, world, port, q, emulate_rccl=False):
+    """Three data-parallel update paths on the same two steps, and gradient accumulation.
+    emulate_rccl: dp's RCCL-only branches (native AVG, BackwardAdam waiting on works[b] with no
+    scale) over gloo through tests/_rccl_emulation.py."""
     import faulthandler
     import sys
     faulthandler.dump_traceback_later(280, exit=True, file=sys.stderr)
@@ -167,6 +169,9 @@ def _variants_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from ml_music_style_transfer_amd import _lib, dp
+    if emulate_rccl:
+        import _rccl_emulation
+        dp = _rccl_emulation.install()
     from ml_music_style_transfer_amd import engine as E
     from ml_music_style_transfer_amd.model import PerformanceNet
     from ml_music_style_transfer_amd.train import make_optimizer
@@ -229,19 +234,23 @@ def _variants_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_dp_update_paths_bitwise_two_ranks_one_gpu(cuda):
+@pytest.mark.parametrize("emulate_rccl", [False, True])
+def test_dp_update_paths_bitwise_two_ranks_one_gpu(cuda, emulate_rccl):
     """Two ranks over gloo on one GPU exercise every data-parallel branch bench.py and train.main
     take over RCCL: the overlapped bucket reducer with Adam in step(), BackwardAdam (each bucket's
     update on a side stream right after that bucket's average, inside backward) and the
     post-backward all-reduce. After two steps all three hold bitwise the same parameters, on
     both ranks. With two backward passes before the exchange the overlapped reducer's result
-    equals the average of the accumulated gradients (fp32 rounding: 1e-5 relative)."""
+    equals the average of the accumulated gradients (fp32 rounding: 1e-5 relative).
+    With emulate_rccl the same holds on the branches only RCCL takes (ReduceOp.AVG issued,
+    BackwardAdam's side stream waiting on works[b] with no scale of its own)."""
     import numpy as np
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_variants_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_variants_worker, args=(r, world, port, q, emulate_rccl))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -216,3 +216,13 @@ def test_multiscale_spectral_loss_rejects_bad_sizes(cuda):
         spectral.multiscale_spectral_loss(x, x, sizes=(48,))
     with pytest.raises(ValueError):
         spectral.multiscale_spectral_loss(x, x, sizes=(2048,))   # needs L > n/2
+
+
+def test_mss_op_without_grad_refuses_backward(cuda):
+    """torch.ops.mst.mss_loss(with_grad=False) on a pred that requires grad: backward raises
+    instead of silently leaving pred.grad empty."""
+    p, q = _mss_pair(1, 4000, 3)
+    pt = torch.from_numpy(p).to(cuda).requires_grad_(True)
+    loss, _ = torch.ops.mst.mss_loss(pt, torch.from_numpy(q).to(cuda), [256, 64], 1.0, 1e-7, False)
+    with pytest.raises(RuntimeError, match="with_grad"):
+        loss.backward()

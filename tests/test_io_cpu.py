@@ -280,3 +280,20 @@ def test_malformed_inputs_raise_valueerror(tmp_path):
     (tmp_path / "c.wav").write_bytes(wav)
     with pytest.raises(ValueError):
         wavio.load(str(tmp_path / "c.wav"))
+
+
+def test_preprocess_zip_data_dir(tmp_path):
+    """preprocess.py:204-210: a zip -data-dir is extracted and replaced by its root directory;
+    a plain directory passes through."""
+    import zipfile
+    from ml_music_style_transfer_amd import preprocess as PP
+    zpath = tmp_path / "style_transfer_train.zip"
+    with zipfile.ZipFile(zpath, "w") as zf:
+        zf.writestr("style_transfer_train/2308_prelude18_mixcraft.mid", b"MThd")
+        zf.writestr("style_transfer_train/2308_prelude18_harpsichord.wav", b"RIFF")
+    out = tmp_path / "x"
+    out.mkdir()
+    d = PP.resolve_data_dir(str(zpath), extract_to=str(out))
+    assert d == str(out / "style_transfer_train")
+    assert sorted(os.listdir(d)) == ["2308_prelude18_harpsichord.wav", "2308_prelude18_mixcraft.mid"]
+    assert PP.resolve_data_dir(d) == d

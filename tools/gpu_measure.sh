@@ -37,6 +37,11 @@ for what in "$@"; do
         python3 bench_aux.py --workload mss --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcmss_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmcmss_write" -o run -- \
         python3 bench_aux.py --workload mss --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcmss_write.log" 2>&1 ;;
+    micro)
+      make -C tools/micro > "$OUT/micro_build.log" 2>&1
+      timeout -k 10 60 tools/micro/permlane_check > "$OUT/permlane_check.txt" 2>&1
+      timeout -k 10 120 tools/micro/store_pattern > "$OUT/store_pattern.txt" 2>&1
+      timeout -k 10 120 tools/micro/stft_stamps > "$OUT/stft_stamps.txt" 2>&1 ;;
     aux)
       timeout -k 10 400 python -u bench_aux.py > "$OUT/bench_aux.jsonl" 2> "$OUT/bench_aux.err" ;;
     layers)
