@@ -319,8 +319,8 @@ __device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
 // values (direct), split-K slab `split`, or (slab != nullptr) a stream-K partial tile.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
 __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS], int m_t,
-                                          int n_t, int kt0, int kt1, int split, float* slab) {
-  const int tid = threadIdx.x;
+                                          int n_t, int kt0, int kt1, int split, float* slab,
+                                          int tid) {
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -694,7 +694,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
     const int kt0 = (int)((long long)split * p.nk / p.splitk);
     const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
-    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, nullptr);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x);
     return;
   }
   const int v = xcd_order(blockIdx.x, gridDim.x);
@@ -709,10 +709,81 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     tile_of(t, nx, ny, m_t, n_t);
     float* slab = (kt0 == 0 && kt1 == p.nk) ? nullptr
                                             : p.ws + (long long)(2 * v + slot) * (BM * BN);
-    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, 0, slab);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, 0, slab, threadIdx.x);
     it += kt1 - kt0;
     slot = 1;
   }
+}
+
+// __syncthreads() calls of one tile_pass over K tiles [kt0, kt1): one per pipelined run (its
+// prologue), two per K tile, three in the epilogue.
+template <bool WG>
+__device__ __forceinline__ int pass_barriers(const GP& p, int kt0, int kt1) {
+  static_assert(MST_GEMM_X6 == 2, "two barriers per K tile");
+  int n = 3;
+  if constexpr (!WG) {
+    if (kt0 < kt1) n += 1 + 2 * (kt1 - kt0);
+  } else {
+    for (int c = 0; c < p.ncls; ++c) {
+      const int kb = max(kt0, p.cstart[c]), ke = min(kt1, p.cstart[c + 1]);
+      if (kb < ke) n += 1 + 2 * (ke - kb);
+    }
+  }
+  return n;
+}
+
+// Ping-pong schedule (round 3, default for split-K / data-parallel grids): one 512-thread
+// workgroup per CU holds two 256-thread groups, each running tile_pass on its own (tile, split)
+// with its own 64 KB LDS region, exactly as two 256-thread workgroups would. The difference is
+// that tile_pass's __syncthreads() now spans both groups, and group 1 enters one barrier later
+// than group 0: while group 0 runs a K tile's MFMAs, group 1 splits and stores its next tile into
+// LDS, and the other way round, on every SIMD (each holds one wave of each group). Two
+// independent workgroups drift into running the same phase at once (both MFMA, then both VALU);
+// here the barrier enforces the alternation. Both groups execute the same barrier sequence (same
+// GEMM, same K range length); an odd last virtual workgroup runs a tile of rows past M (all
+// loads out of range, no stores).
+template <int TAPS, bool WG, int AMODE, bool DUAL>
+__global__ __launch_bounds__(2 * NTHR, 1) void gemm_pp_kernel(const GP p) {
+  __shared__ __attribute__((aligned(16))) float lds[2][LDS_FLOATS];
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  const int g = threadIdx.x >> 8;
+  const int Wv = nx * ny * p.splitk;           // virtual (256-thread) workgroups
+  const int Wr = (Wv + 1) >> 1;                // real workgroups = gridDim.x
+  const int vw = 2 * xcd_order(blockIdx.x, Wr) + g;
+  int m_t, n_t, split = 0, kt0 = 0, kt1 = p.nk;
+  if (vw < Wv) {
+    split = vw / (nx * ny);
+    tile_of(vw - split * nx * ny, nx, ny, m_t, n_t);
+    kt0 = (int)((long long)split * p.nk / p.splitk);
+    kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
+  } else {  // the partner of an odd last group: same K range length as split 0, rows past M
+    m_t = ny;
+    n_t = 0;
+    kt1 = (int)((long long)p.nk / p.splitk);
+  }
+  // barrier counts of this group's pass and of its partner's: the shorter one pads at the end
+  // (K ranges of two splits can differ by a tile, and a weight-gradient range can cross a
+  // different number of K classes)
+  int pk0 = 0, pk1 = (int)((long long)p.nk / p.splitk);
+  const int pv = vw ^ 1;
+  if (pv < Wv) {
+    const int ps = pv / (nx * ny);
+    pk0 = (int)((long long)ps * p.nk / p.splitk);
+    pk1 = (int)((long long)(ps + 1) * p.nk / p.splitk);
+  }
+  const int mine = pass_barriers<WG>(p, kt0, kt1) + 1, theirs = pass_barriers<WG>(p, pk0, pk1) + 1;
+  if (g == 1) __syncthreads();  // enter one phase behind group 0
+  tile_pass<TAPS, WG, AMODE, DUAL>(p, lds + g, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x & (NTHR - 1));
+  if (g == 0) __syncthreads();  // ... and leave with the same barrier count
+  for (int i = mine; i < theirs; ++i) __syncthreads();
+}
+
+static bool gemm_pp() {  // MST_GEMM_PP=1: the ping-pong kernel (A/B; measured slower, see DESIGN)
+  static const bool v = [] {
+    const char* e = getenv("MST_GEMM_PP");
+    return e && e[0] == '1';
+  }();
+  return v;
 }
 
 // Stream-K fixup: one workgroup per (tile, quarter of its rows). A tile finished in place
@@ -884,8 +955,15 @@ int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   if (p.sk_L > 0) grid = dim3((unsigned)((p.sk_I + p.sk_L - 1) / p.sk_L), 1, 1);
   dim3 block(NTHR);
+  const bool pp = p.sk_L == 0 && gemm_pp();
+  const dim3 pgrid((unsigned)((grid.x * grid.y * grid.z + 1) / 2)), pblock(2 * NTHR);
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
-  if (!WG && p.dual)                                                                 \
+  if (pp) {                                                                          \
+    if (!WG && p.dual)                                                               \
+      hipLaunchKernelGGL((gemm_pp_kernel<TP, WG, AM, !WG>), pgrid, pblock, 0, st, p); \
+    else                                                                             \
+      hipLaunchKernelGGL((gemm_pp_kernel<TP, WG, AM, false>), pgrid, pblock, 0, st, p); \
+  } else if (!WG && p.dual)                                                          \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, !WG>), grid, block, 0, st, p);       \
   else                                                                               \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, false>), grid, block, 0, st, p);

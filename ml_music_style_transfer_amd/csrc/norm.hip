@@ -305,9 +305,22 @@ __global__ __launch_bounds__(256) void loss_final_kernel(const double* __restric
 }
 
 // Adam (torch.optim.Adam, single-tensor formulation): m.lerp_(g, 1-b1); v = v*b2 + (1-b2) g^2;
-// p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps). Vectorised 4-wide over the flat buffer.
+// p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps). Vectorised 4-wide over the flat buffer; UNR float4
+// groups per thread per grid-stride step (all loads issued before the arithmetic, so UNR x 4
+// 16-byte loads are in flight per lane). NT: nontemporal loads/stores (streamed once).
 // hyper (nullable, device) = {lr/bc1, sqrt(bc2)} overrides the by-value pair: a captured
 // hipGraph replays one launch whose step-dependent factors the graph itself computes.
+template <int UNR, bool NT>
+__device__ __forceinline__ f32x4 adam_ld(const f32x4* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int UNR, bool NT>
+__device__ __forceinline__ void adam_st(f32x4 v, f32x4* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <int UNR, bool NT>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    long long n, float lr_step, float b2, float w1,
@@ -317,36 +330,89 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
     lr_step = hyper[0];
     bc2_sqrt = hyper[1];
   }
-  long long n4 = n >> 2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    // streamed once: nontemporal loads/stores keep the 20 GB/step stream out of the caches
-    f32x4 pv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(p) + i);
-    f32x4 gv = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g) + i);
-    f32x4 mv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(m) + i);
-    f32x4 vv = __builtin_nontemporal_load(reinterpret_cast<f32x4*>(v) + i);
+  const long long n4 = n >> 2;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  f32x4* P = reinterpret_cast<f32x4*>(p);
+  const f32x4* G = reinterpret_cast<const f32x4*>(g);
+  f32x4* M = reinterpret_cast<f32x4*>(m);
+  f32x4* V = reinterpret_cast<f32x4*>(v);
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += UNR * stride) {
+    f32x4 pv[UNR], gv[UNR], mv[UNR], vv[UNR];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      mv[k] = mv[k] + w1 * (gv[k] - mv[k]);
-      vv[k] = vv[k] * b2 + w2 * (gv[k] * gv[k]);
-      float den = sqrtf(vv[k]) / bc2_sqrt + eps;
-      pv[k] = pv[k] - lr_step * (mv[k] / den);
+    for (int u = 0; u < UNR; ++u) {
+      const long long i = i0 + u * stride;
+      if (UNR == 1 || i < n4) {
+        pv[u] = adam_ld<UNR, NT>(P + i);
+        gv[u] = adam_ld<UNR, NT>(G + i);
+        mv[u] = adam_ld<UNR, NT>(M + i);
+        vv[u] = adam_ld<UNR, NT>(V + i);
+      }
     }
-    __builtin_nontemporal_store(pv, reinterpret_cast<f32x4*>(p) + i);
-    __builtin_nontemporal_store(mv, reinterpret_cast<f32x4*>(m) + i);
-    __builtin_nontemporal_store(vv, reinterpret_cast<f32x4*>(v) + i);
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const long long i = i0 + u * stride;
+      if (UNR > 1 && i >= n4) break;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mv[u][k] = mv[u][k] + w1 * (gv[u][k] - mv[u][k]);
+        vv[u][k] = vv[u][k] * b2 + w2 * (gv[u][k] * gv[u][k]);
+        float den = sqrtf(vv[u][k]) / bc2_sqrt + eps;
+        pv[u][k] = pv[u][k] - lr_step * (mv[u][k] / den);
+      }
+      adam_st<UNR, NT>(pv[u], P + i);
+      adam_st<UNR, NT>(mv[u], M + i);
+      adam_st<UNR, NT>(vv[u], V + i);
+    }
   }
   // tail
   long long i = (n4 << 2) + (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (blockIdx.x == 0 && i < n) {
-    float gv = g[i], mv = m[i], vv = v[i];
-    mv = mv + w1 * (gv - mv);
-    vv = vv * b2 + w2 * (gv * gv);
-    float den = sqrtf(vv) / bc2_sqrt + eps;
-    p[i] = p[i] - lr_step * (mv / den);
-    m[i] = mv;
-    v[i] = vv;
+    float gs = g[i], ms = m[i], vs = v[i];
+    ms = ms + w1 * (gs - ms);
+    vs = vs * b2 + w2 * (gs * gs);
+    float den = sqrtf(vs) / bc2_sqrt + eps;
+    p[i] = p[i] - lr_step * (ms / den);
+    m[i] = ms;
+    v[i] = vs;
   }
+}
+
+// A/B knob (read once): MST_ADAM_VARIANT = "<unroll><n|p>" (nontemporal / plain), default 2n
+// (tools/adam_micro.py over the bench's 726 M parameters: 1n 3.83 ms, 2n 3.52 ms, 4n 3.86 ms,
+// 2p 4.05 ms at 16384 workgroups; profiles/r03/adam_micro_m1.jsonl); MST_ADAM_BLOCKS caps the
+// default grid (16384)
+struct AdamCfg {
+  int unr = 2;
+  bool nt = true;
+  int blocks = 16384;
+};
+static const AdamCfg& adam_cfg() {
+  static const AdamCfg c = [] {
+    AdamCfg r;
+    if (const char* e = getenv("MST_ADAM_VARIANT")) {
+      if (e[0] >= '1' && e[0] <= '4') r.unr = e[0] - '0';
+      if (e[0] && e[1] == 'p') r.nt = false;
+    }
+    if (const char* e = getenv("MST_ADAM_BLOCKS")) r.blocks = atoi(e) > 0 ? atoi(e) : r.blocks;
+    return r;
+  }();
+  return c;
+}
+static void launch_adam(dim3 grid, hipStream_t st, float* p, const float* g, float* m, float* v,
+                        long long n, float lr_step, float b2, float w1, float w2, float eps,
+                        float bc2_sqrt, const float* hyper) {
+  const AdamCfg& c = adam_cfg();
+#define MST_ADAM_L(U, NTF) hipLaunchKernelGGL((adam_kernel<U, NTF>), grid, dim3(256), 0, st, p, g, m, v, n, lr_step, b2, w1, w2, eps, bc2_sqrt, hyper)
+  if (c.nt) {
+    if (c.unr == 1) MST_ADAM_L(1, true);
+    else if (c.unr == 2) MST_ADAM_L(2, true);
+    else MST_ADAM_L(4, true);
+  } else {
+    if (c.unr == 1) MST_ADAM_L(1, false);
+    else if (c.unr == 2) MST_ADAM_L(2, false);
+    else MST_ADAM_L(4, false);
+  }
+#undef MST_ADAM_L
 }
 
 __global__ void scale_kernel(float* x, long long n, float s) {
@@ -551,9 +617,8 @@ int mst_adam_ex_f32(float* p, const float* g, float* m, float* v, int64_t n, flo
                     int32_t max_blocks, void* stream) {
   MST_REQUIRE(p && g && m && v && n > 0 && max_blocks > 0);
   MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, max_blocks)), dim3(256), 0,
-                     (hipStream_t)stream, p, g, m, v, (long long)n, lr_step, b2, one_minus_b1,
-                     one_minus_b2, eps, bc2_sqrt, (const float*)nullptr);
+  launch_adam(dim3(grid_for(n / 4 + 1, 256, max_blocks)), (hipStream_t)stream, p, g, m, v,
+              (long long)n, lr_step, b2, one_minus_b1, one_minus_b2, eps, bc2_sqrt, nullptr);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
@@ -562,9 +627,8 @@ int mst_adam_dev_f32(float* p, const float* g, float* m, float* v, int64_t n, co
                      float b2, float one_minus_b1, float one_minus_b2, float eps, void* stream) {
   MST_REQUIRE(p && g && m && v && hyper && n > 0);
   MST_REQUIRE(((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) % 16 == 0);
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n / 4 + 1, 256, 16384)), dim3(256), 0,
-                     (hipStream_t)stream, p, g, m, v, (long long)n, 0.f, b2, one_minus_b1,
-                     one_minus_b2, eps, 1.f, hyper);
+  launch_adam(dim3(grid_for(n / 4 + 1, 256, adam_cfg().blocks)), (hipStream_t)stream, p, g, m, v,
+              (long long)n, 0.f, b2, one_minus_b1, one_minus_b2, eps, 1.f, hyper);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
@@ -572,7 +636,7 @@ int mst_adam_dev_f32(float* p, const float* g, float* m, float* v, int64_t n, co
 int mst_adam_f32(float* p, const float* g, float* m, float* v, int64_t n, float lr_step, float b2,
                  float one_minus_b1, float one_minus_b2, float eps, float bc2_sqrt, void* stream) {
   return mst_adam_ex_f32(p, g, m, v, n, lr_step, b2, one_minus_b1, one_minus_b2, eps, bc2_sqrt,
-                         16384, stream);
+                         adam_cfg().blocks, stream);
 }
 
 int mst_scale_f32(float* x, int64_t n, float s, void* stream) {
