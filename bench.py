@@ -147,7 +147,7 @@ def aux_legs(world, rank, dev, cpu):
     training step (bench_aux.py's legs, shortened; one-thread oracle CPU baselines)."""
     import bench_aux
     a = argparse.Namespace(steps=10, warmup=2, clips=256, pairs=32, no_cpu_baseline=not cpu,
-                           parallel_cpu=False, no_parity=False)
+                           parallel_cpu=False, no_parity=False, strict=False)
     out = {}
     for fn in (bench_aux.frontend, bench_aux.griffinlim, bench_aux.mss):
         for ln in fn(a, world, rank, dev):

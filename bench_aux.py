@@ -205,13 +205,24 @@ def _cpu_parallel_rate(name, clips):
             "sample": f"{len(clips)} clips, multiprocessing pool of {procs} spawned workers"}
 
 
+def _verdict(ok, msg, args):
+    """Outcome of a sampled oracle check: bench_aux.py run on its own stops on a miss
+    (--strict, the default); bench.py records it in the leg's "parity" object instead, so a
+    miss is reported in the measured line rather than costing the whole bench."""
+    if not ok:
+        if getattr(args, "strict", True):
+            raise AssertionError(msg)
+        print("PARITY MISS: " + msg, file=sys.stderr, flush=True)
+    return {"ok": bool(ok)} if ok else {"ok": False, "miss": msg}
+
+
 def _sampled(B):
     """Clips checked against the oracle after the timed region: one per residue mod 8 (the
     persistent STFT kernel's XCD groups) and the last clip."""
     return sorted({min(B - 1, 9 * r) for r in range(8)} | {B - 1})
 
 
-def _frontend_parity(name, out, x):
+def _frontend_parity(name, out, x, args):
     """Sampled clips of the measured output vs oracle/spectral_ref (tolerances of
     tests/test_gpu_config2.py: log-power 1e-4 absolute, mel 1e-4 of the frame's peak)."""
     from oracle import spectral_ref as SR
@@ -226,8 +237,8 @@ def _frontend_parity(name, out, x):
             err = float((np.abs(out[b] - ref) / (ref.max(axis=0, keepdims=True) + 1e-12)).max())
             tol = 1e-4
         worst = max(worst, err)
-    assert worst <= tol, f"{name}: sampled clips differ from the oracle by {worst} > {tol}"
-    return {"clips": idx, "max_err": worst, "tol": tol, "ok": True}
+    return {"clips": idx, "max_err": worst, "tol": tol,
+            **_verdict(worst <= tol, f"{name}: sampled clips differ from the oracle by {worst} > {tol}", args)}
 
 
 def frontend(args, world, rank, dev):
@@ -262,7 +273,7 @@ def frontend(args, world, rank, dev):
                     cpu["parallel"] = {"error": repr(e)[:200]}
         extra = {"kernel_ms": round(kms, 4)}
         if rank == 0 and not args.no_parity:
-            extra["parity"] = _frontend_parity(name, fn().cpu().numpy(), x)
+            extra["parity"] = _frontend_parity(name, fn().cpu().numpy(), x, args)
         res.append(_line(f"STFT {name} clips/s, 256 x 4 s @ 16 kHz", world * B / dt, "clips/s", world,
                          args.steps, args.warmup, dt * 1e3,
                          {"workload": f"config 2 front end: {name}", "clips_per_gpu": B, "L": L,
@@ -272,21 +283,22 @@ def frontend(args, world, rank, dev):
     return res
 
 
-def _gl_parity(S, y, idx, n_iter):
+def _gl_parity(S, y, idx, n_iter, args):
     """Spectral convergence of sampled clips of the measured output vs the oracle's Griffin-Lim
     from the same (all-ones) init: within 2 % (tests/test_gpu_config2.py's bound)."""
     from ml_music_style_transfer_amd import spectral
     from oracle import spectral_ref as SR
-    rows = []
+    rows, ok, miss = [], True, ""
     for b in idx:
         Sb = S[b].cpu().double().numpy()
         sc = spectral.spectral_convergence(S[b:b + 1], y[b:b + 1], hop=bench.HOP)
         yr = SR.griffinlim(Sb, n_iter=n_iter, hop=bench.HOP)
         sc_ref = float(np.linalg.norm(np.abs(SR.stft(yr, 2048, bench.HOP, out_dtype=None)) - Sb)
                        / np.linalg.norm(Sb))
-        assert sc <= sc_ref * 1.02 + 1e-4, f"Griffin-Lim clip {b}: convergence {sc} vs oracle {sc_ref}"
+        if not sc <= sc_ref * 1.02 + 1e-4:
+            ok, miss = False, f"Griffin-Lim clip {b}: convergence {sc} vs oracle {sc_ref}"
         rows.append({"clip": b, "spectral_convergence": round(sc, 6), "oracle": round(sc_ref, 6)})
-    return {"clips": rows, "tol": "sc <= 1.02 sc_oracle + 1e-4", "ok": True}
+    return {"clips": rows, "tol": "sc <= 1.02 sc_oracle + 1e-4", **_verdict(ok, miss, args)}
 
 
 def griffinlim(args, world, rank, dev):
@@ -316,7 +328,7 @@ def griffinlim(args, world, rank, dev):
                                          "(NumPy float64, 1 thread), scaled to 60 iterations"}
     extra = {"kernel_ms": round(kms, 3)}
     if rank == 0 and not args.no_parity:
-        extra["parity"] = _gl_parity(S, fn(), [0, B - 1], n_iter)
+        extra["parity"] = _gl_parity(S, fn(), [0, B - 1], n_iter, args)
     return [_line("Griffin-Lim clips/s (60 iterations), 256 x 4 s @ 16 kHz", world * B / dt,
                   "clips/s", world, steps, 1, dt * 1e3,
                   {"workload": "config 2 Griffin-Lim, 60 iterations, momentum 0.99", "clips_per_gpu": B,
@@ -324,6 +336,17 @@ def griffinlim(args, world, rank, dev):
                   _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
                         "gl_synth_kernel (atomic seams) + stft_fm_kernel<COMPLEX> per iteration",
                         B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, extra)]
+
+
+def _torch_fp32_mss_gap(p, t, sizes, ref):
+    """Relative gap of torch's fp32 CPU multi-scale loss (torch.stft) to the float64 oracle."""
+    pt, qt, tot = torch.tensor(p), torch.tensor(t), 0.0
+    for n in sizes:
+        w = torch.hann_window(n, periodic=True)
+        a = torch.stft(pt, n, n // 4, window=w, center=True, pad_mode="reflect", return_complex=True).abs()
+        b = torch.stft(qt, n, n // 4, window=w, center=True, pad_mode="reflect", return_complex=True).abs()
+        tot += ((a - b).abs().mean() + (torch.log(a + 1e-7) - torch.log(b + 1e-7)).abs().mean()).item()
+    return abs(tot - ref) / abs(ref)
 
 
 def mss(args, world, rank, dev):
@@ -364,9 +387,15 @@ def mss(args, world, rank, dev):
         ref, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
                                                   tgt[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
         rel = abs(l0.item() - ref) / abs(ref)
-        assert rel <= 1e-4, f"multi-scale loss of pair 0: {l0.item()} vs oracle {ref}"
+        # the piano target has exact silence (11 % of pair 0's samples) and bins far below fp32
+        # resolution, which log(S + 1e-7) amplifies: torch's own fp32 path misses float64 by
+        # ~1e-3 here, so the bar is max(1e-4, 1.5 x that gap) (tests/test_gpu_spectral.py)
+        gap = _torch_fp32_mss_gap(p0.detach()[0].cpu().numpy(), tgt[0].cpu().numpy(), sizes, ref)
+        tol = max(1e-4, 1.5 * gap)
         extra["parity"] = {"pair": 0, "loss": l0.item(), "oracle": ref, "rel_err": rel,
-                           "tol": 1e-4, "ok": True}
+                           "torch_fp32_rel_err": gap, "tol": tol,
+                           **_verdict(rel <= tol, f"multi-scale loss of pair 0: {l0.item()} vs "
+                                                  f"oracle {ref} (rel {rel:.2e} > {tol:.2e})", args)}
     return [_line("multi-scale spectral loss fwd+grad clip-pairs/s, 10 s @ 22.05 kHz, 6 FFT sizes",
                   world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
@@ -384,6 +413,8 @@ def main():
     ap.add_argument("--clips", type=int, default=256)
     ap.add_argument("--pairs", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strict", dest="strict", action="store_false",
+                    help="record a sampled-check miss in the line instead of stopping")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the sampled-clip oracle check after the timed region")
     args = ap.parse_args()

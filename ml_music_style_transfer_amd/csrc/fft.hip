@@ -1941,221 +1941,29 @@ int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, flo
 
 
 // ---------------------------------------------------------------------------
-// Multi-scale spectral loss, n = 1024 (mss.hip has the other sizes and the plan): the same
-// ownership, frame pairing and overlap-add as mss_wave_kernel, but each frame's transform is
-// fft1024_v2 in registers (z = w (p + i q) at n = lane + 64 j; permlane exchanges and one LDS
-// transpose, twiddles from the LDS tables) instead of five in-place LDS radix-4 stages. The
-// bins f and 1024 - f that P_f = (Z_f + conj Z_{n-f}) / 2 pairs sit in lanes l and 64 - l
-// (registers j and 15 - j), exchanged with ds_bpermute; the inverse transform of the packed
-// gradient spectra C is conj(fft1024_v2(conj C)), and C's upper half is routed back the same
-// way. The result goes to the wave's LDS buffer for the workgroup's ordered overlap-add.
+// Multi-scale spectral loss, n = 2048 (mss.hip has the other sizes and the plan): the same
+// ownership, frame pairing and ordered overlap-add as mss_wave_kernel, with every transform a
+// register-resident fft1024_v2.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int mss_reflect(int i, int L) {
   i = i < 0 ? -i : i;
   return i >= L ? 2 * (L - 1) - i : i;
 }
 
-__global__ __launch_bounds__(256, 3) void mss_fft1024_kernel(const MssArgs a) {
-  constexpr int N = 1024, H = N / 4, HALF = N / 2, W = 4, OWN = MSS_RWIN / 256;
-  __shared__ __attribute__((aligned(16))) c2 buf[W * SCR];  // per wave: FFT scratch, then G
-  __shared__ __attribute__((aligned(16))) FftTabs tb;
-  __shared__ float hw[N];
-  __shared__ float red[2][W];
-  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int L = (int)a.L;
-  const float* p = a.pred + (long long)b * a.L;
-  const float* q = a.target + (long long)b * a.L;
-  const bool grad = a.dpred != nullptr;
-  {
-    const float4* src = reinterpret_cast<const float4*>(&kFftTabs);
-    float4* dst = reinterpret_cast<float4*>(&tb);
-    for (int i = tid; i < TAB_F4; i += 256) dst[i] = src[i];
-    // periodic Hann 0.5 - 0.5 cos(2 pi n / 1024) = sin^2(pi n / 1024) = Im(W2048^n)^2
-    for (int n = tid; n < N; n += 256) {
-      const float2 e = kFftTabs.p[n & 511];
-      const float s = (n < 512) ? e.y : e.x;  // W2048^(512 + r) = -i W2048^r
-      hw[n] = s * s;
-    }
-  }
-  __syncthreads();
-  const int own_lo = w * MSS_RWIN;
-  const int f_own0 = w * (MSS_RWIN / H), f_own1 = min(f_own0 + MSS_RWIN / H, a.T);
-  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
-  c2* S = buf + wave * SCR;
-  float acc[OWN];
-#pragma unroll
-  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
-  float s_abs = 0.f, s_log = 0.f;
-
-#pragma unroll 1
-  for (int t_round = f_lo; t_round < f_own1; t_round += 2 * W) {
-    const int t_base = t_round + 2 * wave;  // this wave's frame pair
-    if (t_base < f_own1) {                  // wave-uniform
-      int tid2 = tid;
-      __asm__ volatile("" : "+v"(tid2));
-      const int lane = tid2 & 63;
-      const int src = ((64 - lane) & 63) * 4;  // bperm partner: lane 64 - l
-      c2 zga[9], zgb[9];                      // gradient spectra at f = l + 64 j (j < 8), 512
-#pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        const int t = t_base + pass;
-        const bool valid = t < f_own1;
-        c2 v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int n = lane + 64 * j;
-          v[j] = mk(0.f, 0.f);
-          if (valid) {
-            const int sidx = mss_reflect(t * H + n - HALF, L);
-            v[j] = mk(hw[n] * p[sidx], hw[n] * q[sidx]);
-          }
-        }
-        fft1024_v2(v, S, tb, lane);  // v[j] = Z[l + 64 j]
-        c2 zg[9];
-        c2 prev = v[0];
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          c2 zf, zr;
-          if (j < 8) {
-            const c2 bpj = mk(bperm(src, v[15 - j].x), bperm(src, v[15 - j].y));
-            zr = lane == 0 ? prev : bpj;  // lane 0: Z[1024 - 64 j] is its own register 16 - j
-            prev = bpj;
-            zf = v[j];
-          } else {
-            zf = zr = v[8];  // f = 512 (meaningful in lane 0)
-          }
-          if (j < 8 && lane == 0 && j > 0) zr = v[16 - j];
-          const c2 P = (zf + conj(zr)) * 0.5f;
-          const c2 D = zf - conj(zr);
-          const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
-          const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
-          const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
-          const float lp = __log2f(sp + a.eps) * 0.69314718055994531f;
-          const float lt = __log2f(st + a.eps) * 0.69314718055994531f;
-          const bool bin = j < 8 || lane == 0;  // f = 512 only once
-          c2 g2 = mk(0.f, 0.f);
-          if (valid && bin) {
-            if (t >= f_own0) {
-              s_abs += fabsf(sp - st);
-              s_log += fabsf(lp - lt);
-            }
-            if (grad && sp > 0.f) {
-              const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
-              const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
-              g2 = P * (g * __builtin_amdgcn_rcpf(sp));
-            }
-          }
-          zg[j] = g2;
-        }
-#pragma unroll
-        for (int j = 0; j < 9; ++j) {
-          if (pass == 0) zga[j] = zg[j];
-          else zgb[j] = zg[j];
-        }
-      }
-      if (grad) {
-        // C = H^a + i H^b: c[f] into register j, c[1024 - f] to lane 64 - l, register 15 - j
-        c2 v[16];
-        c2 cn[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const c2 za = zga[j], zb = zgb[j];
-          const bool dc = lane == 0 && j == 0;  // f = 0: real parts only
-          v[j] = dc ? mk(za.x, zb.x) : mk(0.5f * (za.x - zb.y), 0.5f * (za.y + zb.x));
-          cn[j] = mk(0.5f * (za.x + zb.y), 0.5f * (-za.y + zb.x));
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const c2 r = mk(bperm(src, cn[j].x), bperm(src, cn[j].y));
-          v[15 - j] = r;
-        }
-        if (lane == 0) {  // lane 0 holds c[64 r] for every r: c[512], and c[1024 - 64 j] from itself
-          v[8] = mk(zga[8].x, zgb[8].x);
-#pragma unroll
-          for (int j = 1; j < 8; ++j) v[16 - j] = cn[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = conj(v[j]);
-        fft1024_v2(v, S, tb, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the FFT's transpose reads of S are done
-#pragma unroll
-        for (int j = 0; j < 16; ++j) S[lane + 64 * j] = conj(v[j]);  // G[n]: frame a in x, b in y
-      }
-    }
-    if (!grad) continue;
-    __syncthreads();
-    const int r_hi = min(t_round + 2 * W, f_own1);
-#pragma unroll
-    for (int i = 0; i < OWN; ++i) {
-      const int sp = own_lo + tid + 256 * i;
-      const int th = sp / H;
-      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
-      float vv = acc[i];
-      for (int t = t0; t <= t1; ++t) {
-        const int j = sp - t * H;
-        const int rel = t - t_round, ww = rel >> 1;
-        const c2 g = buf[ww * SCR + j];
-        vv += hw[j] * ((rel & 1) ? g.y : g.x);
-      }
-      acc[i] = vv;
-    }
-    __syncthreads();
-  }
-
-  s_abs = wave_sum(s_abs);
-  s_log = wave_sum(s_log);
-  if ((tid & 63) == 0) {
-    red[0][wave] = s_abs;
-    red[1][wave] = s_log;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float sa = 0.f, sl = 0.f;
-    for (int i = 0; i < W; ++i) {
-      sa += red[0][i];
-      sl += red[1][i];
-    }
-    a.partial[((long long)b * a.nwg + w) * 2] = sa;
-    a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
-  }
-  if (!grad) return;
-  float* dp = a.dpred + (long long)b * a.L;
-  float* ed = a.edges + (long long)b * N;
-  const int own_hi = min(own_lo + MSS_RWIN, L + N);
-#pragma unroll
-  for (int i = 0; i < OWN; ++i) {
-    const int pp = own_lo + tid + 256 * i;
-    if (pp >= own_hi) continue;
-    const float vv = acc[i];
-    const int x = pp - HALF;
-    if (x < 0) ed[pp] = vv;
-    else if (x >= L) ed[HALF + (x - L)] = vv;
-    else dp[x] = a.accumulate ? dp[x] + vv : vv;
-  }
-}
-
-
-// n = 2048: a 2048-point transform as one radix-2 step plus two fft1024_v2 (even and odd output
-// bins, z at n = lane + 64 j, j < 32, 32 complex per lane). Forward (decimation in frequency):
-// E = FFT1024(z[n] + z[n + 1024]) = X[2k], O = FFT1024((z[n] - z[n + 1024]) W2048^n) = X[2k + 1].
-// The partner of X[2k] is X[2048 - 2k] = E[1024 - k] (lane 64 - l, register 15 - j) and of
-// X[2k + 1] is X[2047 - 2k] = O[1023 - k] (lane 63 - l, register 15 - j). The inverse runs the
-// other way (decimation in time): g = IFFT1024(c_even) + W2048^-n IFFT1024(c_odd), so the packed
-// gradient spectra are built directly in the even / odd layouts. The window comes from the
-// twiddle table (0.5 - 0.5 Re W2048^n), keeping LDS at 76 KB (two workgroups per CU).
-__device__ __forceinline__ c2 w2048(const FftTabs& tb, int n) {  // W2048^n, 0 <= n < 1024
-  const float2 e = tb.p[n & 511];
-  return n < 512 ? mk(e.x, e.y) : mk(e.y, -e.x);  // W^(512 + r) = -i W^r
-}
-
-// loss terms and gradient spectrum of one bin from Z_f (zf) and Z_(n-f) (zr)
-__device__ __forceinline__ c2 mss_bin(c2 zf, c2 zr, bool use, bool own, bool grad, const MssArgs& a,
-                                      float& s_abs, float& s_log) {
-  const c2 P = (zf + conj(zr)) * 0.5f;
-  const c2 D = zf - conj(zr);
-  const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
+// n = 2048: each frame of pred and of target is a real 2048-point transform, computed as the
+// STFT does it: fft1024_v2 of z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1] (n = lane + 64 j), then the
+// real-FFT post-twist pairing bins k = l + 64 j and 1024 - k (partner Z in lane 64 - l, register
+// 15 - j, by ds_bpermute). Pred and target are never packed into one complex signal: that leaves
+// the target's spectrum with rounding noise of the pred's size, and a silent target then moves
+// log(S + eps) (tools/mss_probe.py). The gradient frame g = Re sum_f Y_f e^(2 pi i f m / 2048)
+// (Y Hermitian, Y_f = G_f / 2 for 0 < f < 1024, real Y_0, Y_1024) is one 1024-point inverse:
+// z[n] = g[2n] + i g[2n+1] = IDFT1024(Z'), Z'_k = A + i e^(i pi k / 1024) B with
+// A = Y_k + conj Y_(1024-k), B = Y_k - conj Y_(1024-k); Z'_(1024-k) = conj A + i conj(e B) goes to
+// lane 64 - l, register 15 - j (lane 0 keeps its own). Frames a and b of a pair then sit in the
+// wave's LDS buffer as (g_a, g_b) for the workgroup's ordered overlap-add. Three fft1024_v2 per
+// frame, as in the packed form this replaces.
+__device__ __forceinline__ c2 mss_term(c2 P, c2 Q, bool use, bool own, bool grad, const MssArgs& a,
+                                       float& s_abs, float& s_log) {
   const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
   const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
   c2 g2 = mk(0.f, 0.f);
@@ -2171,6 +1979,25 @@ __device__ __forceinline__ c2 mss_bin(c2 zf, c2 zr, bool use, bool own, bool gra
     }
   }
   return g2;
+}
+
+// 2 X[k] and 2 conj X[1024 - k] for k = l + 64 j (j < 8) from Z in v (power_pairs_v2's pairing)
+__device__ __forceinline__ void real_pairs(const c2 v[16], const FftTabs& tb, int lane, int src,
+                                           c2 xk[8], c2 xm[8]) {
+  c2 prev = v[0];  // lane 0's partner 1024 - 64 j is its own v[16 - j] (v[0] for j = 0)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const c2 bpj = mk(bperm(src, v[15 - j].x), bperm(src, v[15 - j].y));
+    const c2 Bq = lane == 0 ? prev : bpj;
+    prev = bpj;
+    const c2 A = v[j];
+    const c2 E = mk(A.x + Bq.x, A.y - Bq.y);
+    const c2 D = mk(A.y + Bq.y, Bq.x - A.x);  // -i (A - conj(Bq))
+    const float2 w = tb.p[lane + 64 * j];
+    const c2 TD = cmul(mk(w.x, w.y), D);
+    xk[j] = (E + TD) * 0.5f;     // X[k]
+    xm[j] = conj(E - TD) * 0.5f;  // X[1024 - k]
+  }
 }
 
 __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
@@ -2212,85 +2039,74 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
       int tid2 = tid;
       __asm__ volatile("" : "+v"(tid2));
       const int lane = tid2 & 63;
-      const int src_e = ((64 - lane) & 63) * 4, src_o = (63 - lane) * 4;
-      c2 zae[9], zao[8], zbe[9], zbo[8];  // gradient spectra: even bins 2k (k = l + 64 j, 512), odd 2k + 1
+      const int src = ((64 - lane) & 63) * 4;  // bperm partner: lane 64 - l
+      c2 za[16];                               // frame a's gradient samples (g[2n], g[2n + 1])
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
         const int t = t_base + pass;
         const bool valid = t < f_own1;
-        c2 ve[16], vo[16];
+        c2 vp[16], vq[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int n = lane + 64 * j;
-          c2 x0 = mk(0.f, 0.f), x1 = mk(0.f, 0.f);
+          vp[j] = vq[j] = mk(0.f, 0.f);
           if (valid) {
-            const int s0 = mss_reflect(t * H + n - HALF, L), s1 = mss_reflect(t * H + n + 1024 - HALF, L);
-            const float h0 = hann(n), h1 = hann(n + 1024);
-            x0 = mk(h0 * p[s0], h0 * q[s0]);
-            x1 = mk(h1 * p[s1], h1 * q[s1]);
+            const int s0 = t * H + 2 * n - HALF;
+            const int i0 = mss_reflect(s0, L), i1 = mss_reflect(s0 + 1, L);
+            const float h0 = hann(2 * n), h1 = hann(2 * n + 1);
+            vp[j] = mk(h0 * p[i0], h1 * p[i1]);
+            vq[j] = mk(h0 * q[i0], h1 * q[i1]);
           }
-          ve[j] = x0 + x1;
-          vo[j] = cmul(x0 - x1, w2048(tb, n));
         }
-        fft1024_v2(ve, S, tb, lane);  // ve[j] = X[2 (l + 64 j)]
-        fft1024_v2(vo, S, tb, lane);  // vo[j] = X[2 (l + 64 j) + 1]
+        fft1024_v2(vp, S, tb, lane);  // Z_pred[l + 64 j]
+        fft1024_v2(vq, S, tb, lane);  // Z_target[l + 64 j]
         const bool own = t >= f_own0;
-        c2 prev = ve[0];
+        c2 pk[8], pm[8], qk[8], qm[8], yk[8], ym[8];
+        real_pairs(vp, tb, lane, src, pk, pm);
+        real_pairs(vq, tb, lane, src, qk, qm);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          // even bin f = 2k: partner E[1024 - k] (lane 64 - l, register 15 - j; lane 0: its own 16 - j)
-          const c2 bpe = mk(bperm(src_e, ve[15 - j].x), bperm(src_e, ve[15 - j].y));
-          const c2 zre = lane == 0 ? prev : bpe;
-          prev = bpe;
-          const c2 ge = mss_bin(ve[j], zre, valid, own, grad, a, s_abs, s_log);
-          // odd bin f = 2k + 1: partner O[1023 - k] (lane 63 - l, register 15 - j)
-          const c2 zro = mk(bperm(src_o, vo[15 - j].x), bperm(src_o, vo[15 - j].y));
-          const c2 go = mss_bin(vo[j], zro, valid, own, grad, a, s_abs, s_log);
-          if (pass == 0) { zae[j] = ge; zao[j] = go; } else { zbe[j] = ge; zbo[j] = go; }
+          yk[j] = mss_term(pk[j], qk[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
+          ym[j] = mss_term(pm[j], qm[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
         }
-        // f = 1024 = 2 x 512: E[512], its own partner (lane 0, register 8)
-        const c2 gn = mss_bin(ve[8], ve[8], valid && lane == 0, own, grad, a, s_abs, s_log);
-        if (pass == 0) zae[8] = gn; else zbe[8] = gn;
-      }
-      if (grad) {
-        // c_even[k] = C[2k], c_odd[k] = C[2k + 1], C = H^a + i H^b (H_f = Z_f / 2, H_(n-f) = conj)
-        c2 ce[16], co[16], cne[8], cno[8];
+        // f = 512: X[512] = conj Z[512] (lane 0, register 8)
+        const c2 y512 = mss_term(conj(vp[8]), conj(vq[8]), valid && lane == 0, own, grad, a, s_abs, s_log) * 0.5f;
+        if (!grad) continue;
+        if (lane == 0) {  // Y_0, Y_1024 are real (and G_f / 2 -> G_f there)
+          yk[0] = mk(2.f * yk[0].x, 0.f);
+          ym[0] = mk(2.f * ym[0].x, 0.f);
+        }
+        c2 v[16], cn[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const bool dc = lane == 0 && j == 0;
-          ce[j] = dc ? mk(zae[j].x, zbe[j].x) : mk(0.5f * (zae[j].x - zbe[j].y), 0.5f * (zae[j].y + zbe[j].x));
-          cne[j] = mk(0.5f * (zae[j].x + zbe[j].y), 0.5f * (-zae[j].y + zbe[j].x));
-          co[j] = mk(0.5f * (zao[j].x - zbo[j].y), 0.5f * (zao[j].y + zbo[j].x));
-          cno[j] = mk(0.5f * (zao[j].x + zbo[j].y), 0.5f * (-zao[j].y + zbo[j].x));
+          const c2 A = yk[j] + conj(ym[j]), B = yk[j] - conj(ym[j]);
+          const float2 wk = tb.p[lane + 64 * j];
+          const c2 C = cmul(mk(wk.x, -wk.y), B);  // e^(i pi k / 1024) B
+          v[j] = mk(A.x - C.y, A.y + C.x);         // A + i C
+          cn[j] = mk(A.x + C.y, -A.y + C.x);       // conj A + i conj C
         }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          // C[2048 - 2k] = c_even[1024 - k]: to lane 64 - l, register 15 - j
-          ce[15 - j] = mk(bperm(src_e, cne[j].x), bperm(src_e, cne[j].y));
-          // C[2047 - 2k] = c_odd[1023 - k]: to lane 63 - l, register 15 - j
-          co[15 - j] = mk(bperm(src_o, cno[j].x), bperm(src_o, cno[j].y));
-        }
-        if (lane == 0) {  // c_even[512] = C[1024]; c_even[1024 - 64 j] from itself
-          ce[8] = mk(zae[8].x, zbe[8].x);
+        for (int j = 0; j < 8; ++j) v[15 - j] = mk(bperm(src, cn[j].x), bperm(src, cn[j].y));
+        if (lane == 0) {  // lane 0 holds Z'_(64 r): Z'_512 = 2 conj Y_512, Z'_(1024 - 64 j) from itself
+          v[8] = mk(2.f * y512.x, -2.f * y512.y);
 #pragma unroll
-          for (int j = 1; j < 8; ++j) ce[16 - j] = cne[j];
+          for (int j = 1; j < 8; ++j) v[16 - j] = cn[j];
         }
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          ce[j] = conj(ce[j]);
-          co[j] = conj(co[j]);
-        }
-        fft1024_v2(ce, S, tb, lane);  // conj(IFFT1024(c_even)) at n' = l + 64 j
-        fft1024_v2(co, S, tb, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        for (int j = 0; j < 16; ++j) v[j] = conj(v[j]);
+        fft1024_v2(v, S, tb, lane);  // conj(z) at n = l + 64 j
+        if (pass == 0) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int n = lane + 64 * j;
-          const c2 ge = conj(ce[j]);
-          const c2 go = cmul(conj(co[j]), conj(w2048(tb, n)));  // W2048^-n IFFT(c_odd)
-          S[n] = ge + go;
-          S[n + 1024] = ge - go;
+          for (int j = 0; j < 16; ++j) za[j] = conj(v[j]);
+        } else {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();  // the FFT's transpose reads of S are done
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int n = lane + 64 * j;
+            S[2 * n] = mk(za[j].x, v[j].x);       // g_a[2n], g_b[2n]
+            S[2 * n + 1] = mk(za[j].y, -v[j].y);  // g_a[2n + 1], g_b[2n + 1]
+          }
         }
       }
     }
@@ -2347,10 +2163,6 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
 }
 
 }  // namespace
-
-void mss_fft1024_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st) {
-  hipLaunchKernelGGL(mss_fft1024_kernel, dim3(nwg, B), dim3(256), 0, st, a);
-}
 
 void mss_fft2048_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st) {
   hipLaunchKernelGGL(mss_fft2048_kernel, dim3(nwg, B), dim3(256), 0, st, a);

@@ -9,12 +9,11 @@
 //
 // One launch per size. A workgroup owns R = 4096 consecutive samples of one clip's padded
 // signal and computes every frame that overlaps them (3 halo frames recomputed at the left
-// edge), so the gradient is accumulated in LDS and written once: no atomics, no spectra in
-// HBM. Per frame the two real signals are packed as one complex signal z = w (p + i q) and
-// transformed together (P_f = (Z_f + conj Z_{n-f})/2, Q_f = (Z_f - conj Z_{n-f})/2i); the two
-// gradient frames of a frame pair are likewise packed into one Hermitian-completed inverse
-// transform (real part = frame a, imaginary part = frame b). The FFTs are Stockham radix-4
-// (+ one radix-2 stage for odd log2 n) over LDS, 2048 complex per chunk of frames.
+// edge), so the gradient is accumulated on chip and written once: no atomics, no spectra in
+// HBM. Every frame of pred and of target is transformed on its own as a real FFT (an n/2-point
+// complex transform of the even/odd samples plus the post-twist), in place inside one wave;
+// the two gradient frames of a frame pair are packed into one Hermitian-completed inverse
+// transform (real part = frame a, imaginary part = frame b).
 // Deterministic: fixed summation order everywhere; per-size launches accumulate into dpred
 // in stream order, reflect-pad edges are folded in by a final kernel.
 #include <cstdlib>
@@ -25,11 +24,6 @@
 namespace {
 
 constexpr int RWIN = MSS_RWIN;  // padded samples owned per workgroup
-constexpr int CAP = 2048;    // complex values per LDS FFT buffer
-#ifndef MSS_NT
-#define MSS_NT 256
-#endif
-constexpr int NT = MSS_NT;  // threads per workgroup
 
 struct c2 {
   float x, y;
@@ -42,22 +36,6 @@ __device__ __forceinline__ c2 cmul(c2 a, c2 b) {
   return mk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 __device__ __forceinline__ c2 conjc(c2 a) { return mk(a.x, -a.y); }
-
-// exp(-+2 pi i m / n) from a quarter-wave table qt[r] = (cos, -sin)(2 pi r / n), r < n/4.
-template <int LOG2N, bool INV>
-__device__ __forceinline__ c2 twid(const c2* qt, int m) {
-  constexpr int N = 1 << LOG2N, Q = N / 4;
-  m &= N - 1;
-  const int q = m / Q, r = m & (Q - 1);
-  const c2 w = qt[r];
-  c2 o;
-  if (q == 0) o = w;
-  else if (q == 1) o = mk(w.y, -w.x);
-  else if (q == 2) o = mk(-w.x, -w.y);
-  else o = mk(-w.y, w.x);
-  if (INV) o.y = -o.y;
-  return o;
-}
 
 template <bool INV>
 __device__ __forceinline__ void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
@@ -74,209 +52,12 @@ __device__ __forceinline__ void dft4(c2& a0, c2& a1, c2& a2, c2& a3) {
   }
 }
 
-// One Stockham stage (radix R, Ns = product of earlier radices) on `frames` transforms.
-template <int LOG2N, int R, bool INV>
-__device__ __forceinline__ void stage(const c2* src, c2* dst, int Ns, int frames, const c2* qt) {
-  constexpr int N = 1 << LOG2N, NR = N / R;
-  const int total = frames * NR;
-  for (int idx = threadIdx.x; idx < total; idx += NT) {
-    const int fr = idx / NR, j = idx - fr * NR;
-    const c2* s = src + fr * N;
-    c2* d = dst + fr * N;
-    const int k = j & (Ns - 1);
-    const int step = N / (Ns * R);
-    if constexpr (R == 4) {
-      c2 v0 = s[j], v1 = s[j + NR], v2 = s[j + 2 * NR], v3 = s[j + 3 * NR];
-      v1 = cmul(v1, twid<LOG2N, INV>(qt, k * step));
-      v2 = cmul(v2, twid<LOG2N, INV>(qt, 2 * k * step));
-      v3 = cmul(v3, twid<LOG2N, INV>(qt, 3 * k * step));
-      dft4<INV>(v0, v1, v2, v3);
-      const int base = (j - k) * 4 + k;
-      d[base] = v0;
-      d[base + Ns] = v1;
-      d[base + 2 * Ns] = v2;
-      d[base + 3 * Ns] = v3;
-    } else {
-      c2 v0 = s[j], v1 = s[j + NR];
-      v1 = cmul(v1, twid<LOG2N, INV>(qt, k * step));
-      const int base = (j - k) * 2 + k;
-      d[base] = v0 + v1;
-      d[base + Ns] = v0 - v1;
-    }
-  }
-}
-
-// Full FFT of `frames` transforms starting in buf[0]; returns the buffer index holding the result.
-template <int LOG2N, bool INV>
-__device__ int fft(c2* buf0, c2* buf1, int frames, const c2* qt) {
-  c2* b[2] = {buf0, buf1};
-  int cur = 0, Ns = 1;
-#pragma unroll
-  for (int s = 0; s < LOG2N / 2; ++s) {
-    stage<LOG2N, 4, INV>(b[cur], b[cur ^ 1], Ns, frames, qt);
-    __syncthreads();
-    cur ^= 1;
-    Ns *= 4;
-  }
-  if constexpr (LOG2N & 1) {
-    stage<LOG2N, 2, INV>(b[cur], b[cur ^ 1], Ns, frames, qt);
-    __syncthreads();
-    cur ^= 1;
-  }
-  return cur;
-}
-
 __device__ __forceinline__ int reflect(int i, int L) {
   i = i < 0 ? -i : i;
   return i >= L ? 2 * (L - 1) - i : i;
 }
 
-
-template <int LOG2N>
-__global__ __launch_bounds__(NT) void mss_scale_kernel(const MssArgs a) {
-  constexpr int N = 1 << LOG2N, H = N / 4, HALF = N / 2;
-  constexpr int CF = CAP / N;                // frames per chunk
-  constexpr int OWNF = RWIN / H;             // frames starting in the owned range
-  __shared__ c2 bufs[2][CAP];
-  __shared__ c2 qt[N / 4];
-  __shared__ float acc[RWIN];
-  __shared__ float red[2][NT / 64];
-
-  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int L = (int)a.L;
-  const float* p = a.pred + (long long)b * a.L;
-  const float* q = a.target + (long long)b * a.L;
-  const bool grad = a.dpred != nullptr;
-
-  for (int r = tid; r < N / 4; r += NT) {
-    double s, c;
-    sincospi(2.0 * r / N, &s, &c);
-    qt[r] = mk((float)c, (float)-s);
-  }
-  for (int i = tid; i < RWIN; i += NT) acc[i] = 0.f;
-  __syncthreads();
-
-  const int own_lo = w * RWIN;               // padded coordinates
-  const int f_own0 = w * OWNF, f_own1 = min(f_own0 + OWNF, a.T);
-  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
-  float s_abs = 0.f, s_log = 0.f;
-
-  for (int t0 = f_lo; t0 < f_own1; t0 += CF) {
-    const int nf = min(CF, f_own1 - t0);
-    // ---- load + window: z = w (p + i q)
-    for (int e = tid; e < CF * N; e += NT) {
-      const int fi = e / N, j = e - fi * N;
-      c2 z = mk(0.f, 0.f);
-      if (fi < nf) {
-        const int src = reflect((t0 + fi) * H + j - HALF, L);
-        const float wj = 0.5f - 0.5f * twid<LOG2N, false>(qt, j).x;  // periodic Hann
-        z = mk(wj * p[src], wj * q[src]);
-      }
-      bufs[0][e] = z;
-    }
-    __syncthreads();
-    const int fb = fft<LOG2N, false>(bufs[0], bufs[1], CF, qt);
-    const c2* F = bufs[fb];
-    c2* C = bufs[fb ^ 1];
-    // ---- spectra, loss, gradient spectra packed in frame pairs
-    constexpr int NPAIR = CF >= 2 ? CF / 2 : 1;
-    for (int e = tid; e < NPAIR * (HALF + 1); e += NT) {
-      const int m = e / (HALF + 1), f = e - m * (HALF + 1);
-      c2 zg[2];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        const int fi = CF >= 2 ? 2 * m + x : x;
-        zg[x] = mk(0.f, 0.f);
-        if ((CF >= 2 || x == 0) && fi < nf) {
-          const c2 zf = F[fi * N + f], zr = F[fi * N + ((N - f) & (N - 1))];
-          const c2 P = (zf + conjc(zr)) * 0.5f;
-          const c2 D = zf - conjc(zr);
-          const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
-          const float sp = sqrtf(P.x * P.x + P.y * P.y), st = sqrtf(Q.x * Q.x + Q.y * Q.y);
-          const int t = t0 + fi;
-          const float lp = logf(sp + a.eps), lt = logf(st + a.eps);
-          if (t >= f_own0) {
-            s_abs += fabsf(sp - st);
-            s_log += fabsf(lp - lt);
-          }
-          if (grad && sp > 0.f) {
-            const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
-            const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
-            zg[x] = P * (g / sp);
-          }
-        }
-      }
-      if (grad) {
-        c2* c = C + m * N;
-        if (f == 0 || f == HALF) {
-          c[f] = mk(zg[0].x, zg[1].x);
-        } else {
-          // H^a_f = Za/2, H^a_{n-f} = conj(Za)/2 (same for b); C = H^a + i H^b
-          c[f] = mk(0.5f * (zg[0].x - zg[1].y), 0.5f * (zg[0].y + zg[1].x));
-          c[N - f] = mk(0.5f * (zg[0].x + zg[1].y), 0.5f * (-zg[0].y + zg[1].x));
-        }
-      }
-    }
-    if (!grad) {
-      __syncthreads();
-      continue;
-    }
-    __syncthreads();
-    c2* i0 = bufs[fb ^ 1];
-    c2* i1 = bufs[fb];
-    const int ib = fft<LOG2N, true>(i0, i1, NPAIR, qt);
-    const c2* G = ib == 0 ? i0 : i1;
-    // ---- windowed overlap-add into the owned range (each sample by one thread, frames in order)
-    const int span_lo = max(own_lo, t0 * H), span_hi = min(own_lo + RWIN, (t0 + nf - 1) * H + N);
-    for (int pp = span_lo + tid; pp < span_hi; pp += NT) {
-      float v = acc[pp - own_lo];
-      const int rel = pp - t0 * H;
-      int fi0 = rel - N + 1 > 0 ? (rel - N + 1 + H - 1) / H : 0;
-      int fi1 = min(nf - 1, rel / H);
-      for (int fi = fi0; fi <= fi1; ++fi) {
-        const int j = rel - fi * H;
-        const float wj = 0.5f - 0.5f * twid<LOG2N, false>(qt, j).x;
-        const c2 g = CF >= 2 ? G[(fi >> 1) * N + j] : G[j];
-        v += wj * ((CF >= 2 && (fi & 1)) ? g.y : g.x);
-      }
-      acc[pp - own_lo] = v;
-    }
-    __syncthreads();
-  }
-
-  // ---- loss partials
-  s_abs = wave_sum(s_abs);
-  s_log = wave_sum(s_log);
-  if ((tid & 63) == 0) {
-    red[0][tid >> 6] = s_abs;
-    red[1][tid >> 6] = s_log;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    float sa = 0.f, sl = 0.f;
-    for (int i = 0; i < NT / 64; ++i) {
-      sa += red[0][i];
-      sl += red[1][i];
-    }
-    a.partial[((long long)b * a.nwg + w) * 2] = sa;
-    a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
-  }
-  if (!grad) return;
-  // ---- gradient out: interior samples straight to dpred, reflect-pad samples to `edges`
-  float* dp = a.dpred + (long long)b * a.L;
-  float* ed = a.edges + (long long)b * N;
-  const int own_hi = min(own_lo + RWIN, L + N);
-  for (int pp = own_lo + tid; pp < own_hi; pp += NT) {
-    const float v = acc[pp - own_lo];
-    const int i = pp - HALF;
-    if (i < 0) ed[pp] = v;
-    else if (i >= L) ed[HALF + (i - L)] = v;
-    else dp[i] = a.accumulate ? dp[i] + v : v;
-  }
-}
-
-// Wave-local variant (the default): the same ownership (RWIN padded samples per workgroup, 3
-// halo frames) and the same arithmetic, but every transform runs inside one wave, in place in
+// Every transform runs inside one wave, in place in
 // that wave's LDS buffer (a radix-4 stage reads all its inputs into registers, then writes), so
 // no workgroup barrier sits inside an FFT. Per round each wave takes 2 FB consecutive frames:
 // pass A transforms the FB even ones and keeps their gradient spectra in registers, pass B the
@@ -381,6 +162,7 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
   constexpr int OWN = RWIN / 256;            // owned samples per thread
   __shared__ __attribute__((aligned(16))) c2 buf[W * BW];
   __shared__ c2 qt[N / 4];
+  __shared__ c2 qth[N / 8];  // quarter table of the n/2-point forward transforms
   __shared__ float hw[N];
   __shared__ float red[2][W];
 
@@ -394,6 +176,11 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
     double sn, cs;
     sincospi(2.0 * r / N, &sn, &cs);
     qt[r] = mk((float)cs, (float)-sn);
+  }
+  for (int r = tid; r < N / 8; r += 256) {
+    double sn, cs;
+    sincospi(4.0 * r / N, &sn, &cs);
+    qth[r] = mk((float)cs, (float)-sn);
   }
   for (int j = tid; j < N; j += 256) {
     double sn, cs;
@@ -418,20 +205,25 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
       c2 zga[NE], zgb[NE];
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
-        // load + window FB frames t_base + 2m + pass: z = w (p + i q)
+        // load + window FB frames t_base + 2m + pass, each signal on its own as an n/2-point
+        // complex transform (transform 2m: pred, 2m + 1: target): z_j = w_2j x_2j + i w_2j+1 x_2j+1.
+        // (Packing pred and target into one complex signal, as before, left the target's
+        // spectrum with rounding noise of the pred's size: exact silence in the target came out
+        // as ~1e-6 and log(S + eps) moved the loss by 0.2-1 %, tools/mss_probe.py.)
 #pragma unroll 4
         for (int k = 0; k < BW / 64; ++k) {
-          const int e = lane + 64 * k, m = e / N, j = e - m * N;
-          const int t = t_base + 2 * m + pass;
+          const int e = lane + 64 * k, u = e / HALF, j = e - u * HALF;
+          const int t = t_base + 2 * (u >> 1) + pass;
           c2 z = mk(0.f, 0.f);
           if (t < f_own1) {
-            const int src = reflect(t * H + j - HALF, L);
-            z = mk(hw[j] * p[src], hw[j] * q[src]);
+            const float* x = (u & 1) ? q : p;
+            const int s0 = t * H + 2 * j - HALF;
+            z = mk(hw[2 * j] * x[reflect(s0, L)], hw[2 * j + 1] * x[reflect(s0 + 1, L)]);
           }
           S[e] = z;
         }
         wave_sync();
-        wave_fft<LOG2N, BW, false>(S, qt, lane);
+        wave_fft<LOG2N - 1, BW, false>(S, qth, lane);
         // spectra, loss, gradient spectra (registers)
 #pragma unroll
         for (int jj = 0; jj < NE; ++jj) {
@@ -441,10 +233,16 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
           const int t = t_base + 2 * m + pass;
           c2 zg = mk(0.f, 0.f);
           if (e < FB * NBIN && t < f_own1) {
-            const c2 zf = S[m * N + f], zr = S[m * N + ((N - f) & (N - 1))];
-            const c2 P = (zf + conjc(zr)) * 0.5f;
-            const c2 D = zf - conjc(zr);
-            const c2 Q = mk(D.y * 0.5f, -D.x * 0.5f);
+            // real-FFT post-twist of each signal: X_f = E + W_n^f O, E = (Z_f + conj Z_(n/2-f)) / 2,
+            // O = -i (Z_f - conj Z_(n/2-f)) / 2, indices mod n/2
+            const c2 wf = twq<false>(qt, f, N);
+            const int fa = f & (HALF - 1), fb = (HALF - f) & (HALF - 1);
+            auto bin = [&](const c2* Z) __attribute__((always_inline)) {
+              const c2 A = Z[fa], Bc = conjc(Z[fb]);
+              const c2 E = (A + Bc) * 0.5f, D = A - Bc;
+              return E + cmul(wf, mk(D.y * 0.5f, -D.x * 0.5f));
+            };
+            const c2 P = bin(S + 2 * m * HALF), Q = bin(S + (2 * m + 1) * HALF);
             // hardware sqrt / log2 / rcp (1 ulp): the library forms add ~10 instructions each
             const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
             const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
@@ -600,16 +398,8 @@ __global__ void mss_loss_kernel(const LossArgs a) {
   }
 }
 
-// MST_MSS_LEGACY=1: the workgroup-cooperative kernel (A/B)
-bool mss_legacy() {
-  static const bool v = [] {
-    const char* e = getenv("MST_MSS_LEGACY");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
-
-// MST_MSS_REG=0: n = 1024 on mss_wave_kernel instead of the register-resident FFT (A/B)
+// MST_MSS_REG=0: n = 2048 on mss_wave_kernel instead of the register-resident fft1024_v2
+// kernel (fft.hip; A/B)
 bool mss_reg() {
   static const bool v = [] {
     const char* e = getenv("MST_MSS_REG");
@@ -686,30 +476,16 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     a.edges = w + pl.edge_off[s];
     a.partial = w + pl.part_off[s];
     dim3 grid(pl.nwg[s], (unsigned)B);
-    if (mss_legacy()) {
-      switch (log2i(pl.n[s])) {
-        case 6: mss_scale_kernel<6><<<grid, NT, 0, st>>>(a); break;
-        case 7: mss_scale_kernel<7><<<grid, NT, 0, st>>>(a); break;
-        case 8: mss_scale_kernel<8><<<grid, NT, 0, st>>>(a); break;
-        case 9: mss_scale_kernel<9><<<grid, NT, 0, st>>>(a); break;
-        case 10: mss_scale_kernel<10><<<grid, NT, 0, st>>>(a); break;
-        default: mss_scale_kernel<11><<<grid, NT, 0, st>>>(a); break;
-      }
-    } else {
-      switch (log2i(pl.n[s])) {
-        case 6: mss_wave_kernel<6><<<grid, 256, 0, st>>>(a); break;
-        case 7: mss_wave_kernel<7><<<grid, 256, 0, st>>>(a); break;
-        case 8: mss_wave_kernel<8><<<grid, 256, 0, st>>>(a); break;
-        case 9: mss_wave_kernel<9><<<grid, 256, 0, st>>>(a); break;
-        case 10:
-          if (mss_reg()) mss_fft1024_launch(a, grid.x, grid.y, st);
-          else mss_wave_kernel<10><<<grid, 256, 0, st>>>(a);
-          break;
-        default:
-          if (mss_reg()) mss_fft2048_launch(a, grid.x, grid.y, st);
-          else mss_wave_kernel<11><<<grid, 256, 0, st>>>(a);
-          break;
-      }
+    switch (log2i(pl.n[s])) {
+      case 6: mss_wave_kernel<6><<<grid, 256, 0, st>>>(a); break;
+      case 7: mss_wave_kernel<7><<<grid, 256, 0, st>>>(a); break;
+      case 8: mss_wave_kernel<8><<<grid, 256, 0, st>>>(a); break;
+      case 9: mss_wave_kernel<9><<<grid, 256, 0, st>>>(a); break;
+      case 10: mss_wave_kernel<10><<<grid, 256, 0, st>>>(a); break;
+      default:
+        if (mss_reg()) mss_fft2048_launch(a, grid.x, grid.y, st);
+        else mss_wave_kernel<11><<<grid, 256, 0, st>>>(a);
+        break;
     }
     MST_CHECK_LAUNCH();
   }

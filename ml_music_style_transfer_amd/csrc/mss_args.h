@@ -18,6 +18,5 @@ struct MssArgs {
 };
 
 // n = 1024: grid (nwg, B), 256 threads (fft.hip)
-void mss_fft1024_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st);
 // n = 2048: the same with one radix-2 step around two fft1024 (fft.hip)
 void mss_fft2048_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st);

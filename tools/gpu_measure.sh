@@ -49,11 +49,6 @@ for what in "$@"; do
     msstest)
       timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         -k "multiscale or mss" > "$OUT/pytest_mss.log" 2>&1 ;;
-    abmss)
-      MST_MSS_LEGACY=1 timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_legacy.json" 2>&1
-      timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_wave.json" 2>&1
-      MST_LIB_PATH=ml_music_style_transfer_amd/csrc/build_nt512/libmst_hip.so MST_MSS_LEGACY=1 \
-        timeout -k 10 180 python bench_aux.py --workload mss --no-cpu-baseline --steps 10 --warmup 2 > "$OUT/mss_legacy_nt512.json" 2>&1 ;;
     gltest)
       timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
         -k "griffinlim or istft or stft or mel" > "$OUT/pytest_gl.log" 2>&1 ;;
@@ -152,6 +147,13 @@ for what in "$@"; do
         MST_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_br.jsonl" 2>> "$OUT/ab_br.err"
       done ;;
+    msst)
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_spectral.py -x -v --timeout 120 --timeout-method thread \
+        -k "multiscale or mss" > "$OUT/pytest_mss.log" 2>&1 ;;
+    mssprobe)
+      timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
+    benchnoaux)
+      timeout -k 10 300 python -u bench.py --no-aux > "$OUT/bench_noaux.json" 2> "$OUT/bench_noaux.err" ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;
