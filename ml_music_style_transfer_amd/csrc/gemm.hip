@@ -146,14 +146,65 @@ __device__ __forceinline__ Split3 ld_planes(const __bf16* base, int row, int q) 
   return s;
 }
 
-// Row-major tile units: thread (row, kw) holds k quads rm_quad(kw, u), u = 0..3. The bf16-plane
-// path takes 4 kw + u (a thread's quads adjacent, stored in pairs); the fp32 path kw + 2 u.
-__device__ __forceinline__ constexpr int rm_quad(int kw, int u) {
-  return MST_GEMM_X6 == 2 ? 4 * kw + u : kw + 2 * u;
+// MST_GEMM_X6 == 3: the same bf16 planes, but LDS holds two HALF tiles (16-deep k, 24 KB each,
+// 48 KB with the 64 KB epilogue tile aliasing them): while a wave runs the MFMAs of one half it
+// splits and stores the next half into the other buffer, so the split VALU and the LDS writes
+// sit between its MFMAs instead of in a store phase of their own, and each workgroup barrier
+// ends a phase that holds both. Plane rows are 32 B (two 16-byte quads, swapped when bit 3 of
+// the row is set: the 16-row fragment reads cover all 64 banks). Loader units are laid out so
+// that every thread holds data of both halves (see km_r / km_q / rm_quad).
+constexpr int PLANE_H = BM * 16;  // bf16 elements per half-tile plane
+__device__ __forceinline__ int plh_off(int row, int q) {  // element offset of (row, 16-B quad q)
+  return row * 16 + 8 * (q ^ ((row >> 3) & 1));
+}
+__device__ __forceinline__ void split_store4h(__bf16* plane0, int row, int c, const f32x4 v) {
+  bf16x4 hi, mid, lo;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const Bf3 t = split1(v[i]);
+    hi[i] = t.h;
+    mid[i] = t.m;
+    lo[i] = t.l;
+  }
+  const int off = plh_off(row, c >> 1) + 4 * (c & 1);
+  *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
+  *reinterpret_cast<bf16x4*>(plane0 + PLANE_H + off) = mid;
+  *reinterpret_cast<bf16x4*>(plane0 + 2 * PLANE_H + off) = lo;
+}
+__device__ __forceinline__ void split_store8h(__bf16* plane0, int row, int q, const f32x4 v0,
+                                              const f32x4 v1) {
+  bf16x8 hi, mid, lo;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const Bf3 t = split1(i < 4 ? v0[i] : v1[i - 4]);
+    hi[i] = t.h;
+    mid[i] = t.m;
+    lo[i] = t.l;
+  }
+  const int off = plh_off(row, q);
+  *reinterpret_cast<bf16x8*>(plane0 + off) = hi;
+  *reinterpret_cast<bf16x8*>(plane0 + PLANE_H + off) = mid;
+  *reinterpret_cast<bf16x8*>(plane0 + 2 * PLANE_H + off) = lo;
+}
+__device__ __forceinline__ Split3 ld_planes_h(const __bf16* base, int row, int q) {
+  const __bf16* p = base + plh_off(row, q);
+  Split3 s;
+  s.h = *reinterpret_cast<const bf16x8*>(p);
+  s.m = *reinterpret_cast<const bf16x8*>(p + PLANE_H);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PLANE_H);
+  return s;
 }
 
-constexpr int LDS_NBUF = MST_GEMM_X6 == 2 ? 1 : 2;
-constexpr int LDS_FLOATS = MST_GEMM_X6 == 2 ? BM * BN : (BM + BN) * LDK;
+// Row-major tile units: thread (row, kw) holds 4-float k units rm_quad(kw, u), u = 0..3. The
+// bf16-plane path takes 4 kw + u (a thread's units adjacent, stored in pairs); the half-tile path
+// 2 kw + (u & 1) + 4 (u >> 1) (units 0, 1 in the first 16-deep half, 2, 3 in the second, each
+// pair adjacent); the fp32 path kw + 2 u.
+__device__ __forceinline__ constexpr int rm_quad(int kw, int u) {
+  return MST_GEMM_X6 == 3 ? 2 * kw + (u & 1) + 4 * (u >> 1) : (MST_GEMM_X6 == 2 ? 4 * kw + u : kw + 2 * u);
+}
+
+constexpr int LDS_NBUF = MST_GEMM_X6 >= 2 ? 1 : 2;
+constexpr int LDS_FLOATS = MST_GEMM_X6 >= 2 ? BM * BN : (BM + BN) * LDK;
 
 // acc += a . b over one 16-deep k step, smallest products first
 __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
@@ -335,8 +386,14 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
   // bf16-plane path: see pl_off.
   // A: AMODE 1 (k-contiguous, float4) and 0 (k-scalar) use KM; AMODE 2 (m-contiguous) RM.
   // B: conv/dgrad (n = time, contiguous) RM; wgrad (k = time) KM.
-  const int km_row = tid >> 3;
-  const int km_kq = (tid & 7) * 4;
+  // k-major unit u of this thread: row km_r(u), 4-float k unit km_q(u) (8 lanes along k per row;
+  // half-tile path: 4 lanes per row, units 0, 2 in the first 16-deep half and 1, 3 in the second)
+  auto km_r = [&](int u) __attribute__((always_inline)) {
+    return MST_GEMM_X6 == 3 ? (tid >> 2) + 64 * (u >> 1) : (tid >> 3) + 32 * u;
+  };
+  auto km_q = [&](int u) __attribute__((always_inline)) {
+    return MST_GEMM_X6 == 3 ? (tid & 3) + 4 * (u & 1) : (tid & 7);
+  };
   const int rm_row = tid & 127;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 7);
 
@@ -352,13 +409,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
   uint32_t colb0 = 0, colb1 = 0;
   // wgrad: per-element offsets of the current K class (set per class, see the main loop)
   uint32_t vA[4], vB[4][4];
-  int tlb = 0, bdl = 0;
   if constexpr (!WG) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int m = m0 + (AMODE == 2 ? rm_row : km_row + 32 * u);
-      // KM: the lane's k quad is a fixed channel offset within every tile
-      rowA[u] = m < p.M ? (uint32_t)(m * p.sAm + (AMODE == 2 ? 0 : km_kq * p.sAc)) * 4u : OOB;
+      const int m = m0 + (AMODE == 2 ? rm_row : km_r(u));
+      // KM: the lane's k unit is a fixed channel offset within every tile
+      rowA[u] = m < p.M ? (uint32_t)(m * p.sAm + (AMODE == 2 ? 0 : 4 * km_q(u) * p.sAc)) * 4u : OOB;
     }
     const int n = n0 + rm_row;
     const int bb = n / p.Tn;
@@ -366,17 +422,15 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     tinb = n < p.N ? p.ta * tt + p.tb : -(1 << 29);  // invalid column: every tap out of range
     colb0 = (uint32_t)(bb * p.sb0) * 4u;
     colb1 = DUAL ? (uint32_t)(bb * p.sb1) * 4u : 0u;
-  } else {
-    // wgrad K order: k = (b, t) with the time axis padded to Tp (16, or a multiple of 32), so
-    // a 32-deep tile is one batch row (or two 16-halves when Tp = 16). The lane's k quad (4
-    // consecutive t) sits at time tlb of batch b + bdl.
-    const int q = tid & 7;
-    tlb = 4 * q;
-    if (p.Tp == 16 && q >= 4) {
-      tlb -= 16;
-      bdl = 1;
-    }
   }
+  // wgrad K order: k = (b, t) with the time axis padded to Tp (16, or a multiple of 32), so
+  // a 32-deep tile is one batch row (or two 16-halves when Tp = 16). Unit u's k quad (4
+  // consecutive t) sits at time tl(u) of batch b + bd(u).
+  auto tl = [&](int u) __attribute__((always_inline)) {
+    const int q = km_q(u);
+    return p.Tp == 16 && q >= 4 ? 4 * q - 16 : 4 * q;
+  };
+  auto bd = [&](int u) __attribute__((always_inline)) { return p.Tp == 16 && km_q(u) >= 4 ? 1 : 0; };
   // Per-element offsets of one wgrad K class: every tile of the class shares the time offset
   // t0 - t0ref (a scalar soffset), so range checks against the input and the padding are
   // evaluated once per class here and the tile loop has no per-element work. Invalid elements
@@ -384,10 +438,11 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
   auto wg_class_setup = [&](int t0ref, bool masked) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int m = m0 + km_row + 32 * u;
-      const int n = n0 + km_row + 32 * u;
+      const int m = m0 + km_r(u);
+      const int n = n0 + km_r(u);
       const int c = n / TAPS;  // N order n = c * taps + tap for every output layout
       const int tap = n - c * TAPS;
+      const int tlb = tl(u), bdl = bd(u);
       const int abase = m * p.sPc + bdl * (int)p.sPb + t0ref + tlb;
       const int tin0 = p.ta * (t0ref + tlb) + p.tb + p.tg * tap;  // input time at i = 0
       const int bbase = c * p.sc0 + bdl * (int)p.sb0 + tin0 + p.off0;
@@ -466,9 +521,33 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     }
   };
 
+  // half-tile path: store 16-deep half h of register stage S into LDS half-buffer hb
+  auto store_half = [&](auto S, int h, int hb) __attribute__((always_inline)) {
+    constexpr int st = decltype(S)::value;
+    __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]) + hb * 6 * PLANE_H;
+    __bf16* Bp = Ap + 3 * PLANE_H;
+    if constexpr (AMODE == 2 && !WG) {
+      split_store8h(Ap, rm_row, kw, ra[st][2 * h], ra[st][2 * h + 1]);
+    } else {
+      split_store4h(Ap, km_r(h), tid & 3, ra[st][h]);
+      split_store4h(Ap, km_r(h + 2), tid & 3, ra[st][h + 2]);
+    }
+    if constexpr (WG) {
+      split_store4h(Bp, km_r(h), tid & 3, rb[st][h]);
+      split_store4h(Bp, km_r(h + 2), tid & 3, rb[st][h + 2]);
+    } else {
+      split_store8h(Bp, rm_row, kw, rb[st][2 * h], rb[st][2 * h + 1]);
+    }
+  };
+  (void)store_half;
+
   auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
     constexpr int st = decltype(S)::value;
-#if MST_GEMM_X6 == 2
+#if MST_GEMM_X6 == 3
+    (void)buf;
+    (void)st;
+    return;
+#elif MST_GEMM_X6 == 2
     (void)buf;
     __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]);
     __bf16* Bp = Ap + 3 * PLANE;
@@ -477,11 +556,11 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       for (int u = 0; u < 4; u += 2) split_store8(Ap, rm_row, 2 * kw + u / 2, ra[st][u], ra[st][u + 1]);
     } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) split_store4(Ap, km_row + 32 * u, km_kq / 4, ra[st][u]);
+      for (int u = 0; u < 4; ++u) split_store4(Ap, km_r(u), km_q(u), ra[st][u]);
     }
     if constexpr (WG) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) split_store4(Bp, km_row + 32 * u, km_kq / 4, rb[st][u]);
+      for (int u = 0; u < 4; ++u) split_store4(Bp, km_r(u), km_q(u), rb[st][u]);
     } else {
 #pragma unroll
       for (int u = 0; u < 4; u += 2) split_store8(Bp, rm_row, 2 * kw + u / 2, rb[st][u], rb[st][u + 1]);
@@ -496,13 +575,13 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       if constexpr (AMODE == 2 && !WG)
         *reinterpret_cast<f32x4*>(As + rm_row * LDK + rm_quad(kw, u) * 4) = v;
       else
-        *reinterpret_cast<f32x4*>(As + (km_row + 32 * u) * LDK + km_kq) = v;
+        *reinterpret_cast<f32x4*>(As + km_r(u) * LDK + 4 * km_q(u)) = v;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const f32x4 v = rb[st][u];
       if constexpr (WG)
-        *reinterpret_cast<f32x4*>(Bs + (km_row + 32 * u) * LDK + km_kq) = v;
+        *reinterpret_cast<f32x4*>(Bs + km_r(u) * LDK + 4 * km_q(u)) = v;
       else
         *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + rm_quad(kw, u) * 4) = v;
     }
@@ -524,8 +603,24 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
   // vmcnt(0) between the prefetch and this tile's MFMAs.
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
+  // half-tile path: the 16-deep MFMA step of LDS half-buffer hb
+  auto mfma_half = [&](int hb) __attribute__((always_inline)) {
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]) + hb * 6 * PLANE_H;
+    const __bf16* Bp = Ap + 3 * PLANE_H;
+    const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
+    const Split3 a0 = ld_planes_h(Ap, ra0, h), a1 = ld_planes_h(Ap, ra0 + 32, h);
+    const Split3 b0 = ld_planes_h(Bp, rb0, h), b1 = ld_planes_h(Bp, rb0 + 32, h);
+    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+  };
+  (void)mfma_half;
+
   auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-#if MST_GEMM_X6 == 2
+#if MST_GEMM_X6 == 3
+    (void)buf;
+#elif MST_GEMM_X6 == 2
     // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
     (void)buf;
     const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]);
@@ -591,6 +686,43 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     advance();
     load_tile(I1{}, kb + 1, tap, blk);
     advance();
+#if MST_GEMM_X6 == 3
+    store_half(I0{}, 0, 0);
+    __syncthreads();
+    // Per 32-deep tile kt (register stage sb; stage sb ^ 1 holds tile kt + 1, in flight):
+    //   phase A: MFMAs of kt's first half (buffer 0) | split + store kt's second half -> buffer 1
+    //   phase B: loads of tile kt + 2 into stage sb (free now) | MFMAs of kt's second half
+    //            (buffer 1) | split + store tile kt + 1's first half -> buffer 0
+    // Each phase ends in one barrier; a buffer is written only in the phase after the one that
+    // read it. VALU and LDS writes are placed between the MFMAs (sched_group_barrier).
+    constexpr int NV3 = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
+    auto step = [&](auto S, int kt) __attribute__((always_inline)) {
+      constexpr int sb = decltype(S)::value;
+      mfma_half(0);
+      store_half(S, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // the step's fragment reads
+#pragma unroll
+      for (int i = 0; i < 24; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU (split)
+        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+      __syncthreads();
+      load_tile(S, kt + 2, tap, blk);
+      advance();
+      mfma_half(1);
+      store_half(std::integral_constant<int, sb ^ 1>{}, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+      for (int i = 0; i < 24; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i < NV3) __builtin_amdgcn_sched_group_barrier(0x020, NV3 > 24 ? 2 : 1, 0);  // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+      }
+      __syncthreads();
+    };
+#else
     store_tile(I0{}, 0);
     __syncthreads();
     auto step = [&](auto S, int kt) __attribute__((always_inline)) {
@@ -614,11 +746,14 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
     };
+#endif
     for (int kt = kb; kt < ke; kt += 2) {
       step(I0{}, kt);
       if (kt + 1 < ke) step(I1{}, kt + 1);
     }
   };
+  (void)store_tile;
+  (void)mfma_tile;
   if constexpr (!WG) {
     if (kt0 < kt1) {
       const int tap = kt0 / p.nbT;
@@ -684,6 +819,7 @@ template <int TAPS, bool WG, int AMODE, bool DUAL>
 __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
   static_assert(LDS_NBUF * LDS_FLOATS >= BM * BN, "epilogue tile must fit the A/B buffers");
   static_assert(MST_GEMM_X6 != 2 || 3 * PLANE <= LDS_FLOATS, "bf16 planes must fit");
+  static_assert(MST_GEMM_X6 != 3 || 6 * PLANE_H <= LDS_FLOATS, "two half-tile plane sets must fit");
   __shared__ __attribute__((aligned(16))) float lds[LDS_NBUF][LDS_FLOATS];
   const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
   if (p.sk_L == 0) {
@@ -719,7 +855,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
 // prologue), two per K tile, three in the epilogue.
 template <bool WG>
 __device__ __forceinline__ int pass_barriers(const GP& p, int kt0, int kt1) {
-  static_assert(MST_GEMM_X6 == 2, "two barriers per K tile");
+  static_assert(MST_GEMM_X6 >= 2, "two barriers per K tile");
   int n = 3;
   if constexpr (!WG) {
     if (kt0 < kt1) n += 1 + 2 * (kt1 - kt0);

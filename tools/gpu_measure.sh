@@ -150,6 +150,9 @@ for what in "$@"; do
     msst)
       timeout -k 10 400 python -u -m pytest tests/test_gpu_spectral.py -x -v --timeout 120 --timeout-method thread \
         -k "multiscale or mss" > "$OUT/pytest_mss.log" 2>&1 ;;
+    profmss)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmss" -o run -- \
+        python3 bench_aux.py --workload mss --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$OUT/profmss.json" 2> "$OUT/profmss.err" ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
