@@ -153,6 +153,16 @@ for what in "$@"; do
     profmss)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profmss" -o run -- \
         python3 bench_aux.py --workload mss --no-cpu-baseline --no-parity --steps 5 --warmup 2 > "$OUT/profmss.json" 2> "$OUT/profmss.err" ;;
+    adamab)
+      MST_ADAM_VARIANT=2n timeout -k 10 200 python -u tools/adam_micro.py > "$OUT/adam_micro.jsonl" 2>&1
+      MST_WGRAD_STREAM=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_nows" -o run -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-aux > "$OUT/prof_nows.json" 2> "$OUT/prof_nows.err" ;;
+    abws)
+      for v in 1 0 1 0 1 0; do
+        echo "== MST_WGRAD_STREAM=$v" >> "$OUT/ab_ws.jsonl"
+        MST_WGRAD_STREAM=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_ws.jsonl" 2>> "$OUT/ab_ws.err"
+      done ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
