@@ -203,8 +203,19 @@ __device__ __forceinline__ constexpr int rm_quad(int kw, int u) {
   return MST_GEMM_X6 == 3 ? 2 * kw + (u & 1) + 4 * (u >> 1) : (MST_GEMM_X6 == 2 ? 4 * kw + u : kw + 2 * u);
 }
 
+// MST_GEMM_OCC: resident workgroups per CU. 2 (default): 64 KB of LDS (the epilogue tile) and two
+// register stages. 3 (build-time A/B): the 48 KB of planes only (the epilogue goes through LDS in
+// two 64-row halves), one register stage (tile k+1 loads while tile k's MFMAs run), <= 168 VGPRs.
+#ifndef MST_GEMM_OCC
+#define MST_GEMM_OCC 2
+#endif
+static_assert(MST_GEMM_OCC == 2 || (MST_GEMM_OCC == 3 && MST_GEMM_X6 == 2), "3 workgroups per CU: bf16-plane build only");
+// occupancy per kernel kind: the weight-gradient kernels keep 2 (their per-class element offsets
+// do not fit 168 VGPRs)
+__host__ __device__ constexpr int occ_of(bool wg) { return (MST_GEMM_OCC == 3 && !wg) ? 3 : 2; }
 constexpr int LDS_NBUF = MST_GEMM_X6 >= 2 ? 1 : 2;
-constexpr int LDS_FLOATS = MST_GEMM_X6 >= 2 ? BM * BN : (BM + BN) * LDK;
+constexpr int LDS_FLOATS = MST_GEMM_X6 >= 2 ? BM * BN : (BM + BN) * LDK;  // floats per buffer
+__host__ __device__ constexpr int lds_floats(bool wg) { return occ_of(wg) == 3 ? 3 * PLANE : LDS_FLOATS; }
 
 // acc += a . b over one 16-deep k step, smallest products first
 __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
@@ -368,8 +379,8 @@ __device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
 
 // One pass over K tiles [kt0, kt1) of output tile (m_t, n_t), then the epilogue: the final
 // values (direct), split-K slab `split`, or (slab != nullptr) a stream-K partial tile.
-template <int TAPS, bool WG, int AMODE, bool DUAL>
-__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS], int m_t,
+template <int TAPS, bool WG, int AMODE, bool DUAL, int LF = LDS_FLOATS>
+__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t,
                                           int n_t, int kt0, int kt1, int split, float* slab,
                                           int tid) {
   const int lane = tid & 63;
@@ -628,12 +639,17 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
-      const Split3 a0 = ld_planes(Ap, ra0, 2 * s + h), a1 = ld_planes(Ap, ra0 + 32, 2 * s + h);
       const Split3 b0 = ld_planes(Bp, rb0, 2 * s + h), b1 = ld_planes(Bp, rb0 + 32, 2 * s + h);
-      acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
-      acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
-      acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
-      acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+      {
+        const Split3 a0 = ld_planes(Ap, ra0, 2 * s + h);
+        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+      }
+      {
+        const Split3 a1 = ld_planes(Ap, ra0 + 32, 2 * s + h);
+        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+      }
     }
 #elif MST_GEMM_X6
     // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
@@ -684,8 +700,10 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     };
     load_tile(I0{}, kb, tap, blk);
     advance();
-    load_tile(I1{}, kb + 1, tap, blk);
-    advance();
+    if constexpr (occ_of(WG) != 3) {
+      load_tile(I1{}, kb + 1, tap, blk);
+      advance();
+    }
 #if MST_GEMM_X6 == 3
     store_half(I0{}, 0, 0);
     __syncthreads();
@@ -722,7 +740,36 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       }
       __syncthreads();
     };
+    for (int kt = kb; kt < ke; kt += 2) {
+      step(I0{}, kt);
+      if (kt + 1 < ke) step(I1{}, kt + 1);
+    }
 #else
+    if constexpr (occ_of(WG) == 3) {
+    // one register stage: tile kt + 1 loads during tile kt's MFMAs and is stored after them
+    store_tile(I0{}, 0);
+    __syncthreads();
+    auto step = [&](auto S, int kt) __attribute__((always_inline)) {
+      (void)S;
+      load_tile(I0{}, kt + 1, tap, blk);
+      advance();
+      mfma_tile(0);
+      constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
+      constexpr int PER = 48 / NV > 2 ? 2 : (48 / NV < 1 ? 1 : 48 / NV);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
+      }
+      __syncthreads();
+      store_tile(I0{}, 0);
+      __syncthreads();
+    };
+    for (int kt = kb; kt < ke; kt += 2) {
+      step(I0{}, kt);
+      if (kt + 1 < ke) step(I1{}, kt + 1);
+    }
+    } else {
     store_tile(I0{}, 0);
     __syncthreads();
     auto step = [&](auto S, int kt) __attribute__((always_inline)) {
@@ -746,11 +793,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
       store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
       __syncthreads();
     };
-#endif
     for (int kt = kb; kt < ke; kt += 2) {
       step(I0{}, kt);
       if (kt + 1 < ke) step(I1{}, kt + 1);
     }
+    }
+#endif
   };
   (void)store_tile;
   (void)mfma_tile;
@@ -773,35 +821,43 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
     }
   }
 
-  // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores ----
-  __syncthreads();
-  float* Cs = &lds[0][0];  // 128 x 128 floats (64 KB): the A/B buffers' space
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int nl = wn * 64 + j * 32 + r32;
-        Cs[ml * BN + nl] = acc[i][j][r];
-      }
-  __syncthreads();
+  // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores (EPI_ROWS rows per pass;
+  // with two passes the waves of row half wm write in pass wm) ----
+  constexpr int EPI_ROWS = LF >= BM * BN ? BM : BM / 2;
+  float* Cs = &lds[0][0];  // EPI_ROWS x 128 floats: the A/B buffers' space
   const int nl = tid & (BN - 1);
   const int n = n0 + nl;
-  if (n < p.N) {
-    for (int ml = tid >> 7; ml < BM; ml += NTHR / BN) {
-      const int m = m0 + ml;
-      if (m >= p.M) break;
-      const float v = Cs[ml * BN + nl];
-      if (slab) {
-        slab[ml * BN + nl] = v;
-      } else if (p.splitk > 1) {
-        p.ws[((long long)split * p.M + m) * p.N + n] = v;
-      } else if constexpr (WG) {
-        wgrad_store(p, m, n, v);
-      } else {
-        conv_store(p, m, n, v);
+#pragma unroll
+  for (int ep = 0; ep < BM / EPI_ROWS; ++ep) {
+    __syncthreads();
+    if (EPI_ROWS == BM || wm == ep) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int ml = (EPI_ROWS == BM ? wm * 64 : 0) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int nl2 = wn * 64 + j * 32 + r32;
+            Cs[ml * BN + nl2] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    if (n < p.N) {
+      for (int mr = tid >> 7; mr < EPI_ROWS; mr += NTHR / BN) {
+        const int ml = ep * EPI_ROWS + mr;
+        const int m = m0 + ml;
+        if (m >= p.M) break;
+        const float v = Cs[mr * BN + nl];
+        if (slab) {
+          slab[ml * BN + nl] = v;
+        } else if (p.splitk > 1) {
+          p.ws[((long long)split * p.M + m) * p.N + n] = v;
+        } else if constexpr (WG) {
+          wgrad_store(p, m, n, v);
+        } else {
+          conv_store(p, m, n, v);
+        }
       }
     }
   }
@@ -816,11 +872,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LDS_FLOATS],
 // 2v + 1 (its last), which sk_fixup_kernel sums in workgroup order. Every workgroup then does
 // the same work, so there is no partial last wave.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
-__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
-  static_assert(LDS_NBUF * LDS_FLOATS >= BM * BN, "epilogue tile must fit the A/B buffers");
-  static_assert(MST_GEMM_X6 != 2 || 3 * PLANE <= LDS_FLOATS, "bf16 planes must fit");
-  static_assert(MST_GEMM_X6 != 3 || 6 * PLANE_H <= LDS_FLOATS, "two half-tile plane sets must fit");
-  __shared__ __attribute__((aligned(16))) float lds[LDS_NBUF][LDS_FLOATS];
+__global__ __launch_bounds__(NTHR, occ_of(WG)) void gemm_kernel(const GP p) {
+  constexpr int LF = lds_floats(WG);
+  static_assert(LDS_NBUF * LF >= BM * BN / 2, "epilogue half tile must fit the A/B buffers");
+  static_assert(MST_GEMM_X6 != 2 || 3 * PLANE <= LF, "bf16 planes must fit");
+  static_assert(MST_GEMM_X6 != 3 || 6 * PLANE_H <= LF, "two half-tile plane sets must fit");
+  __shared__ __attribute__((aligned(16))) float lds[LDS_NBUF][LF];
   const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
   if (p.sk_L == 0) {
     const int W = nx * ny * (int)gridDim.z;
@@ -830,7 +887,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
     const int kt0 = (int)((long long)split * p.nk / p.splitk);
     const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
-    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x);
+    tile_pass<TAPS, WG, AMODE, DUAL, LF>(p, lds, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x);
     return;
   }
   const int v = xcd_order(blockIdx.x, gridDim.x);
@@ -845,7 +902,7 @@ __global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
     tile_of(t, nx, ny, m_t, n_t);
     float* slab = (kt0 == 0 && kt1 == p.nk) ? nullptr
                                             : p.ws + (long long)(2 * v + slot) * (BM * BN);
-    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, 0, slab, threadIdx.x);
+    tile_pass<TAPS, WG, AMODE, DUAL, LF>(p, lds, m_t, n_t, kt0, kt1, 0, slab, threadIdx.x);
     it += kt1 - kt0;
     slot = 1;
   }
@@ -1005,14 +1062,14 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
 // a workgroup's time is ~ (its K tiles) x tau. A trailing partial wave of <= 256 workgroups
 // runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave. Split-K
 // adds a slab round trip (s + 2 passes over M x N floats at ~5 TB/s) plus a launch.
-int choose_splitk(int M, int N, int nk, int req) {
+int choose_splitk(int M, int N, int nk, int req, int occ) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
   const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
   static const double tau_env = [] {  // dev override for tuning (MST_SPLITK_TAU seconds)
     const char* e = getenv("MST_SPLITK_TAU");
     return e ? atof(e) : 0.0;
   }();
-  const double slots = 512.0;
+  const double slots = 256.0 * occ;
   const double tau = tau_env > 0 ? tau_env : 3.4e-6;  // s per 32-deep K tile of one workgroup
   static const double bw = [] {  // slab round-trip bandwidth (MST_SPLITK_BW bytes/s, tuning)
     const char* e = getenv("MST_SPLITK_BW");
@@ -1046,7 +1103,7 @@ constexpr int SK_G = 512;
 // GEMMs' HBM-side traffic from 254 to 322 MB per launch (profiles/r01/gemm_traffic_m14_*.json):
 // a workgroup walking several tiles in sequence shares fewer panels through L2 with the
 // workgroups running beside it than one tile per workgroup does.
-void choose_sched(GP& p, int req) {
+void choose_sched(GP& p, int req, bool wg) {
   p.sk_L = p.sk_I = 0;
   const long long tiles = (long long)ceil_div(p.M, BM) * ceil_div(p.N, BN);
   int G = 0;
@@ -1064,7 +1121,7 @@ void choose_sched(GP& p, int req) {
     p.sk_I = tiles * p.nk;
     p.sk_L = (p.sk_I + G - 1) / G;
   } else {
-    p.splitk = choose_splitk(p.M, p.N, p.nk, req);
+    p.splitk = choose_splitk(p.M, p.N, p.nk, req, occ_of(wg));
   }
 }
 
@@ -1230,7 +1287,7 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.drop_p = d->drop_p;
   p.seed = d->seed;
   p.seed_dev = reinterpret_cast<const unsigned long long*>(d->seed_dev);
-  choose_sched(p, d->splitk);
+  choose_sched(p, d->splitk, false);
   return MST_OK;
 }
 
@@ -1307,7 +1364,7 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
-  choose_sched(p, d->splitk);
+  choose_sched(p, d->splitk, true);
   return MST_OK;
 }
 

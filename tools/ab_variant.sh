@@ -1,12 +1,12 @@
 #!/bin/bash
-# GEMM half-tile double-buffer variant (variants/x63, -DMST_GEMM_X6=3) vs the in-tree build:
-# parity tests on the variant, then micro + bench A/B (dev tool; run via gpurun).
+# A GEMM build variant (VAR=variants/<name>/libmst_hip.so, e.g. -DMST_GEMM_X6=3 or -DMST_GEMM_OCC=3)
+# vs the in-tree build: parity tests on the variant, then micro + bench A/B (dev tool; via gpurun).
 set -e -o pipefail
 OUT=gpurun_out/${1:?tag}; mkdir -p "$OUT"
-V=variants/x63/libmst_hip.so
+V=${VAR:-variants/var/libmst_hip.so}
 MST_LIB_PATH=$V timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q \
   --timeout 120 --timeout-method thread -k "gemm or conv or linear or wgrad or golden or bench or splitk or stream" \
-  > "$OUT/pytest_x63.log" 2>&1
+  > "$OUT/pytest_var.log" 2>&1
 echo "parity ok"
 timeout -k 10 300 bash tools/ab_gemm.sh "$OUT/ab_micro.txt" $V
 echo "micro ok"
