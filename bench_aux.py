@@ -401,7 +401,7 @@ def mss(args, world, rank, dev):
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
                    "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
                   _roof(B * bpp / (kms * 1e-3) / 1e9,
-                        "mss_wave_kernel<6..9>, mss_fft1024/2048_kernel + fold + loss reduce",
+                        "mss_wave_kernel<6..10>, mss_fft2048_kernel + fold + loss reduce (pred and target each a real FFT)",
                         B * bpp, traffic=_mss_traffic()), cpu, extra)]
 
 
