@@ -31,6 +31,7 @@ HOP = 256
 T_FRAMES = 252                      # 4.016 s: T = 12 (mod 16) so the U-Net round-trips
 L_SAMPLES = HOP * (T_FRAMES - 1)    # 64,256
 PEAK_FP32_MFMA = 157.3              # TFLOP/s, MI355X_MICROARCH.md (f32 MFMA = vector rate)
+HBM_PEAK_GBS = 8000.0              # GB/s, MI355X_MICROARCH.md (HBM3E)
 PEAK_BF16_MFMA = 2500.0             # TFLOP/s dense, MI355X_MICROARCH.md
 
 
@@ -233,6 +234,8 @@ def main():
         gstep = GraphedTrainStep(model, opt, warmup=1)
 
     graph_on = [True]  # off for the per-launch GEMM timing leg (a replay runs no Python)
+    adam_ev = []       # HIP events around opt.step() in the timed steps (the adam_kernel leg)
+    adam_on = [False]
 
     def step():
         if gstep is not None and graph_on[0]:
@@ -249,7 +252,13 @@ def main():
         loss.backward()               # overlapped bucket all-reduces start inside backward
         if world > 1 and args.no_overlap and comm_on[0]:
             dp.allreduce_gradients(model)
+        if adam_on[0]:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         opt.step()                    # waits for the all-reduce, then the update (or joins it)
+        if adam_on[0]:
+            ev[1].record()
+            adam_ev.append(ev)
         return loss
 
     for _ in range(args.warmup):
@@ -259,8 +268,10 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    adam_on[0] = gstep is None and not args.adam_overlap
     for _ in range(args.steps):
         loss = step()
+    adam_on[0] = False
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -361,6 +372,16 @@ def main():
         },
         "final_loss": round(final_loss, 5),
     }
+    if adam_ev:
+        # the optimizer step of the timed steps (one adam_kernel over the flat buffer, 28 B per
+        # parameter: p, m, v read + written, g read), HIP events on its launch stream
+        n_par = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        a_ms = sum(e0.elapsed_time(e1) for e0, e1 in adam_ev) / len(adam_ev)
+        a_gbs = 28.0 * n_par / (a_ms * 1e-3) / 1e9
+        out["adam"] = {"kernel": "adam_kernel (flat fp32 p/g/m/v, torch.optim.Adam arithmetic)",
+                       "bound": "hbm", "params": n_par, "bytes_per_step": 28 * n_par,
+                       "ms_per_step": round(a_ms, 3), "achieved": round(a_gbs, 1),
+                       "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a_gbs / HBM_PEAK_GBS, 4)}
     if comm is not None:
         out["allreduce"] = comm
     if gstep is not None:

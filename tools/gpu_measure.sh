@@ -163,6 +163,12 @@ for what in "$@"; do
         MST_WGRAD_STREAM=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_ws.jsonl" 2>> "$OUT/ab_ws.err"
       done ;;
+    abprev)
+      for lib in "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_prev.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_prev.jsonl" 2>> "$OUT/ab_prev.err"
+      done ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
