@@ -491,7 +491,10 @@ __global__ __launch_bounds__(512, 4) void stft_kernel(const float* __restrict__ 
 // log1p(p) = log(1 + p) on the hardware log (absolute error <= 1e-6, inside the 1e-4 bar).
 // ---------------------------------------------------------------------------
 #ifndef FM_WAVES
-#define FM_WAVES 8                 // frequency-major STFT: waves per workgroup (8 or 16)
+#define FM_WAVES 8                 // frequency-major STFT: waves per workgroup (8 or 16), mel / complex
+#endif
+#ifndef FM_WAVES_POW
+#define FM_WAVES_POW 16            // ... for log-power / power
 #endif
 constexpr int RSTR_MEL = 130;      // staging row stride for <= 128 mel bands (= 2 mod 32)
 
@@ -1862,7 +1865,11 @@ int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int 
     MST_CHECK_LAUNCH();
     return MST_OK;
   }
-  const bool fm_fits = !(hop & 1) && (long long)((FM_WAVES - 1) * hop + NFFT) * 4 <= (long long)FM_WAVES * (SCR * 8 - NC * 4);
+  // frames per block: 16 (one 1024-thread workgroup per CU, 64-byte row pieces) for the
+  // log-power / power STFT, 8 (two workgroups per CU) for mel and the complex STFT
+  // (profiles/r03/ab_fm16.txt: log-power 0.166 -> 0.162 ms; mel +2 %, Griffin-Lim +8 % at 16)
+  const int fmw = (mode == MODE_LOGPOW || mode == MODE_POWER) ? FM_WAVES_POW : FM_WAVES;
+  const bool fm_fits = !(hop & 1) && (long long)((fmw - 1) * hop + NFFT) * 4 <= (long long)fmw * (SCR * 8 - NC * 4);
   if (mode == MODE_COMPLEX && !(fm_fits && stft_cx_fm())) {  // frame-major (B, T, F, 2), round-1 kernel
     dim3 grid(ceil_div(T, FR), B), block(512);
     hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel);
@@ -1876,21 +1883,23 @@ int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int 
     }
   } else {  // frequency-major: persistent XCD-grouped workgroups over FM_WAVES-frame blocks
     // resident workgroups: 256 CUs x (1024 threads: one, 512: two), i.e. 32 or 64 per XCD group
-    const long long per_group = (long long)ceil_div(B, 8) * ceil_div(T, FM_WAVES);
-    const int wmax = FM_WAVES == 16 ? 32 : 64;
+    const long long per_group = (long long)ceil_div(B, 8) * ceil_div(T, fmw);
+    const int wmax = fmw == 16 ? 32 : 64;
     const int W = (int)(per_group < wmax ? per_group : wmax);
-    dim3 grid(8 * W), block(64 * FM_WAVES);
+    dim3 grid(8 * W), block(64 * fmw);
     const long long rows = mode == MODE_MEL ? mel.n_mels : NB;
     MST_REQUIRE(rows * T * (mode == MODE_COMPLEX ? 8 : 4) < (1ll << 31));  // per-clip buffer descriptors
     const bool v4 = mode == MODE_COMPLEX || ((T & 3) == 0 && ((uintptr_t)out & 15) == 0);
 #define MST_STFT_FM(M, V) hipLaunchKernelGGL((stft_fm_kernel<M, V, FM_WAVES>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W)
+#define MST_STFT_FMP(M, V) hipLaunchKernelGGL((stft_fm_kernel<M, V, FM_WAVES_POW>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W)
     switch (mode) {
-      case MODE_LOGPOW: if (v4) MST_STFT_FM(MODE_LOGPOW, true); else MST_STFT_FM(MODE_LOGPOW, false); break;
-      case MODE_POWER: if (v4) MST_STFT_FM(MODE_POWER, true); else MST_STFT_FM(MODE_POWER, false); break;
+      case MODE_LOGPOW: if (v4) MST_STFT_FMP(MODE_LOGPOW, true); else MST_STFT_FMP(MODE_LOGPOW, false); break;
+      case MODE_POWER: if (v4) MST_STFT_FMP(MODE_POWER, true); else MST_STFT_FMP(MODE_POWER, false); break;
       case MODE_COMPLEX: MST_STFT_FM(MODE_COMPLEX, true); break;
       default: if (v4) MST_STFT_FM(MODE_MEL, true); else MST_STFT_FM(MODE_MEL, false); break;
     }
 #undef MST_STFT_FM
+#undef MST_STFT_FMP
   }
   MST_CHECK_LAUNCH();
   return MST_OK;

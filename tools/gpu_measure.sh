@@ -169,6 +169,24 @@ for what in "$@"; do
         MST_LIB_PATH=$lib timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_prev.jsonl" 2>> "$OUT/ab_prev.err"
       done ;;
+    abfm16)
+      MST_LIB_PATH=variants/fm16/libmst_hip.so timeout -k 10 300 python -u -m pytest tests/test_gpu_spectral.py tests/test_gpu_config2.py \
+        -x -q --timeout 120 --timeout-method thread -k "stft or mel or logpow or process_spectrum" > "$OUT/pytest_fm16.log" 2>&1
+      for lib in "" variants/fm16/libmst_hip.so "" variants/fm16/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_fm16.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload frontend --no-cpu-baseline \
+          >> "$OUT/ab_fm16.jsonl" 2>> "$OUT/ab_fm16.err"
+      done ;;
+    abfm16gl)
+      MST_LIB_PATH=variants/fm16/libmst_hip.so timeout -k 10 400 python -u -m pytest tests/test_gpu_spectral.py tests/test_gpu_config2.py \
+        tests/test_istft_grad.py -x -q --timeout 120 --timeout-method thread > "$OUT/pytest_fm16_all.log" 2>&1
+      for lib in "" variants/fm16/libmst_hip.so "" variants/fm16/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_fm16_gl.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload griffinlim --no-cpu-baseline --no-parity \
+          >> "$OUT/ab_fm16_gl.jsonl" 2>> "$OUT/ab_fm16_gl.err"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload frontend --no-cpu-baseline --no-parity \
+          >> "$OUT/ab_fm16_gl.jsonl" 2>> "$OUT/ab_fm16_gl.err"
+      done ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
