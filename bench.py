@@ -375,7 +375,8 @@ def main():
     if adam_ev:
         # the optimizer step of the timed steps (one adam_kernel over the flat buffer, 28 B per
         # parameter: p, m, v read + written, g read), HIP events on its launch stream
-        n_par = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        n_par = int(model.flat_buffers()[2])  # the flat buffer the kernel streams (the dead MBR
+        # convolutions' weights are not in it)
         a_ms = sum(e0.elapsed_time(e1) for e0, e1 in adam_ev) / len(adam_ev)
         a_gbs = 28.0 * n_par / (a_ms * 1e-3) / 1e9
         out["adam"] = {"kernel": "adam_kernel (flat fp32 p/g/m/v, torch.optim.Adam arithmetic)",
