@@ -216,6 +216,8 @@ def main():
     # update, overlapped with the GEMMs; +1.2 % per step at N=1, but the GEMMs it overlaps run
     # slower, which the roofline leg then reports). Default: one launch in opt.step().
     opt = make_optimizer(model, lr=1e-3, overlap_backward=args.adam_overlap and not args.no_overlap)
+    if os.environ.get("MST_BENCH_PREALLOC", "0") == "1":  # A/B: Adam moments allocated up front
+        opt.prepare()
 
     # synthetic per-rank data, resident in HBM: target clips, style-reference clips, rolls
     tgt_audio, notes = synth_clips(B, 1234 + 1000 * rank)

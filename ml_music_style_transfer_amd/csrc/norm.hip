@@ -252,22 +252,27 @@ __global__ __launch_bounds__(256) void bias_rows_kernel(const float* __restrict_
   db[c] = accumulate ? db[c] + s : s;
 }
 
-// db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one block per channel.
+// db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one wave per channel, four per block. A wave
+// covers 64 / G rows of G-lane segments per step (G = 16, 32 or 64 with G >= T or G = 64), so
+// the short rows of the dense layers (T = 15 at B = 32) keep most lanes busy; lane partials and
+// the wave reduction run in a fixed order (deterministic). The previous form (one 256-thread
+// block per channel, threads along t) left 241 of 256 threads idle at T = 15.
 __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dy, int B, int C,
                                                         int T, float scale, float* __restrict__ db,
                                                         int accumulate) {
-  const int c = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;  // whole wave
+  const int G = T <= 16 ? 16 : (T <= 32 ? 32 : 64);
+  const int R = 64 / G, sub = lane / G, tl = lane - sub * G;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) {
+  for (int b = sub; b < B; b += R) {
     const float* r = dy + ((long long)b * C + c) * T;
-    for (int t = threadIdx.x; t < T; t += blockDim.x) s += r[t];
+    for (int t = tl; t < T; t += G) s += r[t];
   }
-  __shared__ float red[4];
   s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float v = (red[0] + red[1] + red[2] + red[3]) * scale;
+  if (lane == 0) {
+    float v = s * scale;
     if (accumulate) v += db[c];
     db[c] = v;
   }
@@ -545,8 +550,8 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
 int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float scale, float* db,
                       int32_t accumulate, void* stream) {
   MST_REQUIRE(dy && db && B > 0 && C > 0 && T > 0);
-  hipLaunchKernelGGL(bias_grad_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, B, C, T,
-                     scale, db, accumulate);
+  hipLaunchKernelGGL(bias_grad_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, dy, B,
+                     C, T, scale, db, accumulate);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }

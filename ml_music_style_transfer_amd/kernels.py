@@ -318,6 +318,8 @@ def bias_grad_rows(rs, db, accumulate):
 
 
 def bias_grad(dy, db, accumulate):
+    if not dy.is_contiguous() or not db.is_contiguous():
+        raise ValueError("bias_grad: contiguous (B, C, T) dy and (C,) db required")
     B, C, T = dy.shape
     L.check(_lib().mst_bias_grad_f32(L.ptr(dy), B, C, T, 1.0, L.ptr(db), 1 if accumulate else 0,
                                      L.stream()), "bias_grad")

@@ -123,6 +123,20 @@ class Adam(torch.optim.Optimizer):
             self._flat_groups[key] = st
         return st
 
+    def prepare(self):
+        """Allocate the flat moment buffers now instead of at the first step (same values: zeros,
+        or the loaded per-parameter moments). Returns self."""
+        owner = getattr(self, "_owner", None)
+        if owner is None or not owner._flat_ok():
+            return self
+        index = owner._flat["index"]
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if id(p) in index]
+            flat = self._flat_of(group, params) if params else None
+            if flat is not None:
+                self._flat_state(gi, flat[0], params)
+        return self
+
     def load_state_dict(self, state_dict):
         """torch.optim.Optimizer.load_state_dict; the flat moment buffers are rebuilt from the
         loaded per-parameter state on the next step (resume keeps exp_avg/exp_avg_sq/step)."""

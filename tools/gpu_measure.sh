@@ -187,6 +187,17 @@ for what in "$@"; do
         MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload frontend --no-cpu-baseline --no-parity \
           >> "$OUT/ab_fm16_gl.jsonl" 2>> "$OUT/ab_fm16_gl.err"
       done ;;
+    biasab)
+      timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q --timeout 120 \
+        --timeout-method thread > "$OUT/pytest_bias.log" 2>&1
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+        python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-aux > "$OUT/prof_bench.json" 2> "$OUT/prof.err" ;;
+    abprealloc)
+      for v in 0 1 0 1 0 1; do
+        echo "== MST_BENCH_PREALLOC=$v" >> "$OUT/ab_prealloc.jsonl"
+        MST_BENCH_PREALLOC=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
+          >> "$OUT/ab_prealloc.jsonl" 2>> "$OUT/ab_prealloc.err"
+      done ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
