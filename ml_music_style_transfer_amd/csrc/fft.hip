@@ -1983,7 +1983,7 @@ __device__ __forceinline__ c2 mss_term(c2 P, c2 Q, bool use, bool own, bool grad
     }
     if (grad && sp > 0.f) {
       const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
-      const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
+      const float g = sg * (1.f + a.alpha * __builtin_amdgcn_rcpf(sp + a.eps)) * a.inv_cnt;
       g2 = P * (g * __builtin_amdgcn_rcpf(sp));
     }
   }

@@ -70,11 +70,11 @@ __device__ __forceinline__ c2 twq(const c2* qt, int m, int N) {  // W_N^m from t
   m &= N - 1;
   const int Q = N >> 2, q = m / Q, r = m & (Q - 1);
   const c2 w = qt[r];
-  c2 o;
-  if (q == 0) o = w;
-  else if (q == 1) o = mk(w.y, -w.x);
-  else if (q == 2) o = mk(-w.x, -w.y);
-  else o = mk(-w.y, w.x);
+  // times (-i)^q by selects (an if/else chain on the per-lane quadrant compiled to divergent
+  // branches around each lookup)
+  const bool odd = q & 1, neg = q & 2;
+  const float a = odd ? w.y : w.x, b = odd ? -w.x : w.y;
+  c2 o = mk(neg ? -a : a, neg ? -b : b);
   if (INV) o.y = -o.y;
   return o;
 }
@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
             }
             if (grad && sp > 0.f) {
               const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
-              const float g = sg * (1.f + a.alpha / (sp + a.eps)) * a.inv_cnt;
+              const float g = sg * (1.f + a.alpha * __builtin_amdgcn_rcpf(sp + a.eps)) * a.inv_cnt;
               zg = P * (g * __builtin_amdgcn_rcpf(sp));
             }
           }
