@@ -132,24 +132,45 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
   const int Tp = T >> 1;
   float z0[NP], z1[NP], g0[NP], g1[NP];
   float s1 = 0.f, s2 = 0.f;
+  // every load of the row is issued before any is used, from clamped in-row addresses (a
+  // per-element "load or default" branch made the compiler wait vmcnt(0) at each join: five
+  // serialised round trips per row, 2.2 TB/s against the forward kernel's 6.4)
+  // whole-tensor buffer descriptors (wave-uniform: a per-row descriptor is not, and hipcc wraps
+  // each load in a waterfall loop); an absent input (null) reads 0 through the range check;
+  // element indices are clamped into the row and the values past it masked below
+  auto rsrc = [&](const float* base, long long n) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
+                                             base ? (int)(4 * n) : 0, 0x00020000);
+  };
+  const auto ry = rsrc(y, rows * T), ra = rsrc(d_a, rows * T);
+  const auto rp0 = rsrc(dp0, rows * Tp), rp1 = rsrc(dp1, rows * Tp);
+  auto ld = [&](__amdgpu_buffer_rsrc_t rs, long long i) __attribute__((always_inline)) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * i), 0, 0));
+  };
+  const bool has_p = (dp0 || dp1) && Tp > 0;  // kernel-uniform
+  float y0v[NP], y1v[NP], a0v[NP], a1v[NP], gpv[NP];
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 2 * G * q;
-    bool ok0 = i0 < T, ok1 = i0 + 1 < T;
-    float y0 = ok0 ? yr[i0] : mu, y1 = ok1 ? yr[i0 + 1] : mu;
-    z0[q] = (y0 - mu) * r;
-    z1[q] = (y1 - mu) * r;
-    float da0 = 0.f, da1 = 0.f;
-    if (d_a) {
-      if (ok0) da0 = d_a[row * T + i0];
-      if (ok1) da1 = d_a[row * T + i0 + 1];
-    }
-    int pi = i0 >> 1;
-    if ((dp0 || dp1) && pi < Tp) {
-      float gp = (dp0 ? dp0[row * Tp + pi] : 0.f) + (dp1 ? dp1[row * Tp + pi] : 0.f);
-      float a0 = lrelu(z0[q], slope), a1 = lrelu(z1[q], slope);
-      if (a1 > a0) da1 += gp;
-      else da0 += gp;
+    const int i0 = 2 * lane + 2 * G * q;
+    const long long e0 = row * T + (i0 < T ? i0 : 0), e1 = row * T + (i0 + 1 < T ? i0 + 1 : 0);
+    const long long ep = row * Tp + ((i0 >> 1) < Tp ? (i0 >> 1) : 0);
+    y0v[q] = ld(ry, e0);
+    y1v[q] = ld(ry, e1);
+    a0v[q] = ld(ra, e0);
+    a1v[q] = ld(ra, e1);
+    gpv[q] = ld(rp0, ep) + ld(rp1, ep);
+  }
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int i0 = 2 * lane + 2 * G * q;
+    const bool ok0 = i0 < T, ok1 = i0 + 1 < T;
+    z0[q] = ((ok0 ? y0v[q] : mu) - mu) * r;
+    z1[q] = ((ok1 ? y1v[q] : mu) - mu) * r;
+    float da0 = ok0 ? a0v[q] : 0.f, da1 = ok1 ? a1v[q] : 0.f;
+    if (has_p && (i0 >> 1) < Tp) {
+      const float a0 = lrelu(z0[q], slope), a1 = lrelu(z1[q], slope);
+      if (a1 > a0) da1 += gpv[q];
+      else da0 += gpv[q];
     }
     g0[q] = ok0 ? (z0[q] > 0.f ? da0 : da0 * slope) : 0.f;
     g1[q] = ok1 ? (z1[q] > 0.f ? da1 : da1 * slope) : 0.f;
@@ -526,6 +547,7 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
                                int32_t T, float slope, const float* d_a, const float* d_pool0,
                                const float* d_pool1, float* dy, float* rowsum, void* stream) {
   MST_REQUIRE(y && mean && rstd && dy && rows > 0 && T > 1);
+  MST_REQUIRE(rows * (long long)T < (1ll << 29));  // 32-bit buffer byte offsets in in_bwd_kernel
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
