@@ -127,7 +127,6 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
   const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
   const int lane = threadIdx.x & (G - 1);
   if (row >= rows) return;
-  const float* yr = y + row * T;
   const float mu = mean[row], r = rstd[row];
   const int Tp = T >> 1;
   float z0[NP], z1[NP], g0[NP], g1[NP];
