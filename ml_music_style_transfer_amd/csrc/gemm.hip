@@ -305,12 +305,14 @@ __device__ __forceinline__ int xcd_order(int w, int W) {
   return xcd * q + min(xcd, r) + (w >> 3);
 }
 
-__device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
+// bias value bm = p.bias[m] passed in (loaded ahead by the caller: a load inside this per-element
+// path, behind its branches, makes the compiler wait for it element by element)
+__device__ __forceinline__ void conv_store_b(const GP& p, int m, int n, float v, float bm) {
   if (m >= p.M || n >= p.N) return;
   int b = n / p.Tn;
   int t = n - b * p.Tn;
   v *= p.alpha;
-  if (p.bias) v += p.bias[m];
+  if (p.bias) v += bm;
   if (p.act == MST_ACT_RELU) v = fmaxf(v, 0.f);
   else if (p.act == MST_ACT_LRELU) v = v > 0.f ? v : 0.01f * v;
   int to = t * p.ostride + p.ophase;
@@ -333,6 +335,10 @@ __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
     if (p.gt1) v = p.gt1[idx] > 0.f ? v * p.gs1 : 0.f;
     p.y1[idx] = v;
   }
+}
+
+__device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
+  conv_store_b(p, m, n, v, (p.bias && m < p.M) ? p.bias[m] : 0.f);
 }
 
 __device__ __forceinline__ void wgrad_store(const GP& p, int m, int n, float v) {
@@ -827,6 +833,11 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
   float* Cs = &lds[0][0];  // EPI_ROWS x 128 floats: the A/B buffers' space
   const int nl = tid & (BN - 1);
   const int n = n0 + nl;
+  // the tile's bias values, staged once in LDS (read back as broadcasts: a wave's row is
+  // uniform), instead of a dependent global load per stored element
+  __shared__ float s_bias[BM];
+  const bool use_bias = !WG && !slab && p.splitk <= 1 && p.bias != nullptr;
+  if (use_bias && tid < BM) s_bias[tid] = m0 + tid < p.M ? p.bias[m0 + tid] : 0.f;
 #pragma unroll
   for (int ep = 0; ep < BM / EPI_ROWS; ++ep) {
     __syncthreads();
@@ -856,7 +867,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
         } else if constexpr (WG) {
           wgrad_store(p, m, n, v);
         } else {
-          conv_store(p, m, n, v);
+          conv_store_b(p, m, n, v, use_bias ? s_bias[ml] : 0.f);
         }
       }
     }
@@ -1046,10 +1057,22 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
     for (; s < p.splitk; ++s) v += ws[(long long)s * q4 + j];
     int m = (4 * j) / p.N;
     int n = 4 * j - m * p.N;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};  // bias values loaded ahead of the stores
+    if (!WG && p.bias) {
+      int mm = m, nn = n;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bv[e] = p.bias[mm < p.M ? mm : p.M - 1];
+        if (++nn == p.N) {
+          nn = 0;
+          ++mm;
+        }
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       if (WG) wgrad_store(p, m, n, v[e]);
-      else conv_store(p, m, n, v[e]);
+      else conv_store_b(p, m, n, v[e], bv[e]);
       if (++n == p.N) {
         n = 0;
         ++m;

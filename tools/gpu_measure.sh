@@ -163,6 +163,9 @@ for what in "$@"; do
         MST_WGRAD_STREAM=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_ws.jsonl" 2>> "$OUT/ab_ws.err"
       done ;;
+    gemmt)
+      timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_bench_shapes.py -x -q \
+        --timeout 120 --timeout-method thread > "$OUT/pytest_gemm.log" 2>&1 ;;
     abprev)
       for lib in "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so; do
         echo "== lib ${lib:-in-tree}" >> "$OUT/ab_prev.jsonl"
