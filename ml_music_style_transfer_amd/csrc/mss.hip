@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
   __shared__ __attribute__((aligned(16))) c2 buf[W * BW];
   __shared__ c2 qt[N / 4];
   __shared__ c2 qth[N / 8];  // quarter table of the n/2-point forward transforms
-  __shared__ float hw[N];
+  __shared__ __attribute__((aligned(16))) float hw[N];
   __shared__ float red[2][W];
 
   const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -210,17 +210,29 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
         // (Packing pred and target into one complex signal, as before, left the target's
         // spectrum with rounding noise of the pred's size: exact silence in the target came out
         // as ~1e-6 and log(S + eps) moved the loss by 0.2-1 %, tools/mss_probe.py.)
-#pragma unroll 4
-        for (int k = 0; k < BW / 64; ++k) {
-          const int e = lane + 64 * k, u = e / HALF, j = e - u * HALF;
-          const int t = t_base + 2 * (u >> 1) + pass;
-          c2 z = mk(0.f, 0.f);
-          if (t < f_own1) {
+        // Branch-free: a frame past f_own1 loads frame f_own1 - 1 (always in range) and is
+        // zeroed by a select; a load under a per-element branch made hipcc wait for each
+        // element's loads at the join (32 serialised global round trips per round).
+        constexpr int KC = LOG2N >= 10 ? 4 : 8;  // elements per load batch (2 KC loads in flight)
+#pragma unroll
+        for (int k0 = 0; k0 < BW / 64; k0 += KC) {
+          float x0[KC], x1[KC];
+#pragma unroll
+          for (int kk = 0; kk < KC; ++kk) {
+            const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
+            const int t = min(t_base + 2 * (u >> 1) + pass, f_own1 - 1);
             const float* x = (u & 1) ? q : p;
             const int s0 = t * H + 2 * j - HALF;
-            z = mk(hw[2 * j] * x[reflect(s0, L)], hw[2 * j + 1] * x[reflect(s0 + 1, L)]);
+            x0[kk] = x[reflect(s0, L)];
+            x1[kk] = x[reflect(s0 + 1, L)];
           }
-          S[e] = z;
+#pragma unroll
+          for (int kk = 0; kk < KC; ++kk) {
+            const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
+            const bool live = t_base + 2 * (u >> 1) + pass < f_own1;
+            const float2 wj = *reinterpret_cast<const float2*>(hw + 2 * j);
+            S[e] = live ? mk(wj.x * x0[kk], wj.y * x1[kk]) : mk(0.f, 0.f);
+          }
         }
         wave_sync();
         wave_fft<LOG2N - 1, BW, false>(S, qth, lane);

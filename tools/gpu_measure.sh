@@ -201,6 +201,12 @@ for what in "$@"; do
         MST_BENCH_PREALLOC=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_prealloc.jsonl" 2>> "$OUT/ab_prealloc.err"
       done ;;
+    abmssprev)
+      for lib in "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so; do
+        echo "== lib ${lib:-in-tree}" >> "$OUT/ab_mss_prev.jsonl"
+        MST_LIB_PATH=$lib timeout -k 10 200 python -u bench_aux.py --workload mss --no-cpu-baseline --no-parity \
+          --steps 20 --warmup 3 >> "$OUT/ab_mss_prev.jsonl" 2>> "$OUT/ab_mss_prev.err"
+      done ;;
     mssprobe)
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
