@@ -360,21 +360,35 @@ struct FoldArgs {
   long long off[8];
 };
 
-__global__ void mss_fold_kernel(const FoldArgs a) {
-  const int b = blockIdx.x;
+__device__ void mss_fold(const FoldArgs& a, int b) {
   const int L = (int)a.L;
   float* dp = a.dpred + (long long)b * a.L;
-  for (int s = 0; s < a.nsz; ++s) {
+  int maxhalf = 0;
+  for (int s = 0; s < a.nsz; ++s) maxhalf = max(maxhalf, a.n[s] / 2);
+  // head: padded p < n/2 is x[n/2 - p]; tail: x[2(L-1) - (L + k)] = x[L - 2 - k]
+  if (L > 2 * maxhalf + 1) {
+    // head targets [1, maxhalf] and tail targets [L - 1 - maxhalf, L - 2] are disjoint: one
+    // read-modify-write per target, the sizes added in size order as below (same sums)
+    for (int i = threadIdx.x; i < maxhalf; i += blockDim.x) {
+      const int h = i + 1;
+      float vh = dp[h], vt = dp[L - 2 - i];
+      for (int s = 0; s < a.nsz; ++s) {
+        const int half = a.n[s] / 2;
+        const float* ed = a.edges + a.off[s] + (long long)b * a.n[s];
+        if (h <= half) vh += ed[half - h];
+        if (i < half) vt += ed[half + i];
+      }
+      dp[h] = vh;
+      dp[L - 2 - i] = vt;
+    }
+    return;
+  }
+  for (int s = 0; s < a.nsz; ++s) {  // short clips: head and tail overlap
     const int n = a.n[s], half = n / 2;
     const float* ed = a.edges + a.off[s] + (long long)b * n;
-    // head: padded p < n/2 is x[n/2 - p]; tail: x[2(L-1) - (L + k)] = x[L - 2 - k]
-    for (int k = threadIdx.x; k < half; k += blockDim.x) {
-      dp[half - k] += ed[k];
-    }
+    for (int k = threadIdx.x; k < half; k += blockDim.x) dp[half - k] += ed[k];
     __syncthreads();
-    for (int k = threadIdx.x; k < half; k += blockDim.x) {
-      dp[L - 2 - k] += ed[half + k];
-    }
+    for (int k = threadIdx.x; k < half; k += blockDim.x) dp[L - 2 - k] += ed[half + k];
     __syncthreads();
   }
 }
@@ -389,14 +403,25 @@ struct LossArgs {
   float* loss;
 };
 
-__global__ void mss_loss_kernel(const LossArgs a) {
+__device__ void mss_loss(const LossArgs& a) {
   __shared__ double red[4];
   double tot = 0.0;
+  constexpr int U = 8;  // partial pairs in flight per thread (clamped loads, masked adds)
   for (int s = 0; s < a.nsz; ++s) {
     double sa = 0.0, sl = 0.0;
-    for (int i = threadIdx.x; i < a.cnt[s]; i += blockDim.x) {
-      sa += a.partial[a.off[s] + 2 * i];
-      sl += a.partial[a.off[s] + 2 * i + 1];
+    const int cnt = a.cnt[s];
+    const float2* part = reinterpret_cast<const float2*>(a.partial + a.off[s]);
+    for (int i0 = threadIdx.x; i0 < cnt; i0 += U * blockDim.x) {
+      float2 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = part[min(i0 + u * (int)blockDim.x, cnt - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u * (int)blockDim.x < cnt) {
+          sa += v[u].x;
+          sl += v[u].y;
+        }
+      }
     }
     tot += (sa + (double)a.alpha * sl) * (double)a.inv_cnt[s];
   }
@@ -408,6 +433,19 @@ __global__ void mss_loss_kernel(const LossArgs a) {
     for (int i = 0; i < (int)(blockDim.x / 64); ++i) t += red[i];
     a.loss[0] = (float)t;
   }
+}
+
+// One launch after the per-size kernels: blocks 0 .. B-1 fold the edge gradients of clip b,
+// the last block reduces the loss partials.
+struct FinishArgs {
+  FoldArgs f;
+  LossArgs l;
+  int fold_blocks;
+};
+
+__global__ __launch_bounds__(256) void mss_finish_kernel(const FinishArgs a) {
+  if ((int)blockIdx.x < a.fold_blocks) mss_fold(a.f, blockIdx.x);
+  else mss_loss(a.l);
 }
 
 // MST_MSS_REG=0: n = 2048 on mss_wave_kernel instead of the register-resident fft1024_v2
@@ -501,31 +539,27 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     }
     MST_CHECK_LAUNCH();
   }
-  if (dpred) {
-    FoldArgs f;
-    f.dpred = dpred;
-    f.edges = w;
-    f.L = L;
-    f.B = (int)B;
-    f.nsz = pl.nsz;
-    for (int s = 0; s < pl.nsz; ++s) {
-      f.n[s] = pl.n[s];
-      f.off[s] = pl.edge_off[s];
-    }
-    mss_fold_kernel<<<(unsigned)B, 256, 0, st>>>(f);
-    MST_CHECK_LAUNCH();
-  }
-  LossArgs la;
+  FinishArgs fa;
+  fa.fold_blocks = dpred ? (int)B : 0;
+  FoldArgs& f = fa.f;
+  f.dpred = dpred;
+  f.edges = w;
+  f.L = L;
+  f.B = (int)B;
+  f.nsz = pl.nsz;
+  LossArgs& la = fa.l;
   la.partial = w;
   la.nsz = pl.nsz;
   la.alpha = alpha;
   la.loss = loss;
   for (int s = 0; s < pl.nsz; ++s) {
+    f.n[s] = pl.n[s];
+    f.off[s] = pl.edge_off[s];
     la.off[s] = pl.part_off[s];
     la.cnt[s] = (int)(B * pl.nwg[s]);
     la.inv_cnt[s] = (float)(1.0 / ((double)B * pl.T[s] * (pl.n[s] / 2 + 1)));
   }
-  mss_loss_kernel<<<1, 256, 0, st>>>(la);
+  mss_finish_kernel<<<(unsigned)(fa.fold_blocks + 1), 256, 0, st>>>(fa);
   MST_CHECK_LAUNCH();
   return 0;
 }

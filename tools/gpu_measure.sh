@@ -201,6 +201,11 @@ for what in "$@"; do
         MST_BENCH_PREALLOC=$v timeout -k 10 200 python -u bench.py --no-aux --no-cpu-baseline --steps 20 --warmup 3 \
           >> "$OUT/ab_prealloc.jsonl" 2>> "$OUT/ab_prealloc.err"
       done ;;
+    pmcmsssq)
+      timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_ACTIVE_INST_VALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS --output-format csv \
+        -d "$OUT/pmcmss_sq" -o run -- python3 bench_aux.py --workload mss --no-cpu-baseline --no-parity \
+        --steps 2 --warmup 1 > "$OUT/pmcmss_sq.log" 2>&1 ;;
     abmssprev)
       for lib in "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so "" variants/prev/libmst_hip.so; do
         echo "== lib ${lib:-in-tree}" >> "$OUT/ab_mss_prev.jsonl"
