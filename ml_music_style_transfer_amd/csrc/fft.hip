@@ -2159,15 +2159,22 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   float* dp = a.dpred + (long long)b * a.L;
   float* ed = a.edges + (long long)b * N;
   const int own_hi = min(own_lo + MSS_RWIN, L + N);
+  // the previous sizes' sums, loaded together up front (clamped in range; a load inside the
+  // per-sample branch below made hipcc wait for each one: 16 serialised round trips)
+  float prev[OWN];
+#pragma unroll
+  for (int i = 0; i < OWN; ++i)
+    prev[i] = dp[min(max(own_lo + tid + 256 * i - HALF, 0), L - 1)];  // unconditional: no join
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
+    // one store per sample to the address picked by selects (stores under the three-way
+    // branch each waited for every earlier store: vmcnt counts stores on gfx950)
     const int pp = own_lo + tid + 256 * i;
-    if (pp >= own_hi) continue;
-    const float vv = acc[i];
     const int x = pp - HALF;
-    if (x < 0) ed[pp] = vv;
-    else if (x >= L) ed[HALF + (x - L)] = vv;
-    else dp[x] = a.accumulate ? dp[x] + vv : vv;
+    const float v0 = acc[i];
+    float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
+    const float val = (x >= 0 && x < L && a.accumulate) ? prev[i] + v0 : v0;
+    if (pp < own_hi) *dst = val;
   }
 }
 
