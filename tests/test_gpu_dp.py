@@ -295,3 +295,37 @@ def test_bench_aux_two_ranks_one_gpu(tmp_path):
     assert len(lines) == 2
     for ln in lines:
         assert ln["n_gpus"] == 2 and ln["value"] > 0 and ln["config"]["clips_per_gpu"] == 16
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_one_gpu(tmp_path):
+    """bench.py exactly as the driver launches it for N > 1 (python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 ... bench.py --gpus 2), rehearsed with
+    MST_BENCH_BACKEND=gloo so both ranks can share this box's one GPU: rank 0 prints ONE JSON
+    line with n_gpus 2, global batch 2 x 32, "dp2", value = both ranks' frames over the
+    max-over-ranks step time, and an all-reduce object (bus bandwidth, exposed communication)
+    without an error. The numbers are gloo-through-host numbers, NOT xGMI measurements: this only
+    proves the multi-rank bench path runs (the step being sharded is reference
+    model/train.py:129-143)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MST_BENCH_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-aux", "--no-cpu-baseline", "--kernel-timing-steps", "0"]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["steps"] == 2 and ln["warmup"] == 1
+    assert ln["config"]["global_batch"] == 64 and ln["config"]["parallelism"] == "dp2"
+    assert ln["scaling"] == "weak" and ln["value"] > 0
+    assert abs(ln["value"] - 64 * 252 / (ln["ms_per_step"] / 1000.0)) <= 1e-3 * ln["value"]
+    ar = ln["allreduce"]
+    assert "error" not in ar, ar
+    assert ar["bus_GBps"] > 0 and "exposed_comm_ms_per_step" in ar and ar["overlapped"] is True
+    assert ar["grad_bytes"] == 4 * 726_039_425
