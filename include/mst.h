@@ -236,9 +236,8 @@ int mst_onoff_f32(const float* roll, int32_t B, int32_t T, float* bin, float* on
 
 /* library identity / sanity */
 const char* mst_version(void);
-/* MFMA products per fp32 multiply-add in the GEMMs of this build: 6 = bf16x6 (fp32 operands
- * split exactly into three bf16 pieces, six bf16 MFMA products, fp32 accumulation), 1 = fp32
- * MFMA (built with -DMST_GEMM_X6=0). */
+/* MFMA products per fp32 multiply-add in the GEMMs: 6 = bf16x6 (fp32 operands split exactly
+ * into three bf16 pieces, six bf16 MFMA products, fp32 accumulation). */
 int mst_gemm_products(void);
 int mst_device_arch(char* buf, int32_t n); /* writes gcnArchName of the current device */
 

@@ -1012,235 +1012,6 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
     STAMP(6);
   }
 }
-// Frequency-major STFT, warp-specialised (round 3; log-power / power / mel). One 768-thread
-// workgroup per CU: waves 0-7 are compute waves (one frame of each 8-frame block each: window,
-// FFT, post-twist, staging), waves 8-11 are memory waves (span DMA into LDS, write-out of the
-// staged block). With the wave -> SIMD assignment each SIMD holds two compute waves and one memory
-// wave, so the SIMD's vector pipe is fed by the compute waves while the memory waves' LDS reads,
-// DMA and stores run beside them. Per block i two workgroup barriers:
-//   phase 1  compute: read the frame of block i from SP (its DMA was waited for before the
-//                     previous barrier B, as LDS-DMA data is ordered for other waves only by the
-//                     issuing wave's vmcnt followed by a barrier)
-//            memory:  nothing
-//   barrier A: SP is read out
-//   phase 2  compute: window, FFT, post-twist -> staging ST[i & 1] (+ bin 1024 in ny)
-//            memory:  DMA block i + 1's span into SP; read ST[(i - 1) & 1] and store those rows
-//                     (frequency-major (B, F, T), 32-byte row pieces); wait for the DMA
-//   barrier B: ST[i & 1] complete, ST[(i - 1) & 1] read out, block i + 1's span landed
-// LDS: FFT scratch 8 x 8,704 B, staging 2 x 32 KB (+ bin 1024), span 15 KB, tables 12 KB
-// (162,752 B of 163,840). Requires hop <= 256 (span (7 hop + 2048) samples).
-constexpr int WS_CW = 8;   // compute waves (frames per block)
-constexpr int WS_MW = 4;   // memory waves
-constexpr int WS_SP = 7 * 256 + NFFT;  // span samples at hop <= 256
-template <int MODE, bool V4>
-__global__ __launch_bounds__(64 * (WS_CW + WS_MW), 3) void stft_ws_kernel(
-    const float* __restrict__ x, int B, int L, int T, int hop, int pad_mode, float* __restrict__ out,
-    MelTab mel, int W) {
-  constexpr int FPB = WS_CW;
-  __shared__ __attribute__((aligned(16))) c2 scratch[WS_CW * SCR];
-  __shared__ __attribute__((aligned(16))) float st[2][FPB * NC];
-  __shared__ __attribute__((aligned(16))) float ny[2][FPB];
-  __shared__ __attribute__((aligned(16))) float span[WS_SP];
-  __shared__ __attribute__((aligned(16))) FftTabs tb;
-  const int nblk = (T + FPB - 1) / FPB;
-  const int xg = blockIdx.x & 7, wi = blockIdx.x >> 3;
-  const int U = (B - xg + 7) / 8 * nblk;  // blocks of this XCD group
-  if (wi >= U) return;                    // whole workgroup: before any barrier
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  constexpr bool MELM = MODE == MODE_MEL;
-  const int nrows = MELM ? mel.n_mels : NB;
-  const int clip_bytes = nrows * T * 4;  // < 2^31: checked by the launcher
-  const long long rowT = T;
-  const int sp = (FPB - 1) * hop + NFFT;
-  auto clip_of = [&](int u) { return xg + 8 * (u / nblk); };
-  auto frame0_of = [&](int u) { return (u % nblk) * FPB; };
-
-  if (wave >= WS_CW) {
-    // ------------------------------------------------------------------ memory waves
-    const int mw = wave - WS_CW;
-    const int lane = threadIdx.x & 63;
-    const int mt = threadIdx.x - 64 * WS_CW;  // 0 .. 255
-    for (int i = mt; i < TAB_F4; i += 64 * WS_MW)
-      reinterpret_cast<float4*>(&tb)[i] = reinterpret_cast<const float4*>(&kFftTabs)[i];
-    load_span<WS_MW>(x + (long long)clip_of(wi) * L, L, frame0_of(wi) * hop - NFFT / 2, sp, pad_mode,
-                     span, mw, lane);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): block wi's span has landed
-    LDS_BARRIER();                       // prologue barrier: span and tables in LDS
-    constexpr int NIT = MELM ? 1 : 8;    // (row, quad) items per memory thread
-    constexpr int NST = MELM ? 1 : 9;    // stores per thread per block (V4: a fixed count)
-    constexpr int VM_NST = 0x0f70 | (NST & 15) | ((NST >> 4) << 14);  // s_waitcnt vmcnt(NST)
-    int pb = -1, pf0 = 0, pnfr = 0;
-#pragma unroll 1
-    for (int u = wi, it = 0;; u += W, ++it) {
-      const bool have = u < U;
-      STAMP(0);
-      LDS_BARRIER();  // A: the compute waves have read block u's frames out of SP
-      STAMP(1);
-      const int un = u + W;
-      if (have && un < U)
-        load_span<WS_MW>(x + (long long)clip_of(un) * L, L, frame0_of(un) * hop - NFFT / 2, sp,
-                         pad_mode, span, mw, lane);
-      STAMP(2);
-      const int par = (u - wi) / W + 1;  // the previous block's staging buffer: (it - 1) & 1
-      const float* S0 = st[par & 1];
-      const int nr = MELM ? mel.n_mels : NC;
-      float vv[NIT][4];
-#pragma unroll
-      for (int i = 0; i < NIT; ++i) {
-        const int k = (mt >> 1) + 128 * i, q = mt & 1;
-        const int kk = k < nr ? k : 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-          vv[i][w] = MELM ? S0[(4 * q + w) * RSTR_MEL + kk] : S0[stage_pos<FPB>(4 * q + w, kk)];
-      }
-      const float nyv = ny[par & 1][lane & 7];
-      STAMP(3);
-      const float* oc = out + (long long)(pb < 0 ? 0 : pb) * nrows * rowT;
-      if (V4) {
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(oc), (short)0, clip_bytes, 0x00020000);
-#pragma unroll
-        for (int i = 0; i < NIT; ++i) {
-          const int k = (mt >> 1) + 128 * i, q = mt & 1;
-          const bool ok = pb >= 0 && k < nr && 4 * q + 3 < pnfr;
-          const int off = ok ? (int)((k * rowT + pf0 + 4 * q) * 4) : clip_bytes;
-          __builtin_amdgcn_raw_buffer_store_b128(
-              __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
-                                 make_float4(vv[i][0], vv[i][1], vv[i][2], vv[i][3])),
-              rs, off, 0, 0);
-        }
-        if (!MELM) {  // bin 1024 of the block: 8 frames from memory wave 0, lanes 0-7
-          const int off = (pb >= 0 && mw == 0 && lane < pnfr) ? (int)((NC * rowT + pf0 + lane) * 4) : clip_bytes;
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(nyv), rs, off, 0, 0);
-        }
-        __builtin_amdgcn_s_waitcnt(VM_NST);  // the span DMA (issued before the stores) landed
-      } else {
-        if (pb >= 0) {
-          float* ob = const_cast<float*>(oc) + pf0;
-#pragma unroll
-          for (int i = 0; i < NIT; ++i) {
-            const int k = (mt >> 1) + 128 * i, q = mt & 1;
-            if (k < nr)
-              for (int w = 0; w < 4 && 4 * q + w < pnfr; ++w) ob[(long long)k * rowT + 4 * q + w] = vv[i][w];
-          }
-          if (!MELM && mw == 0 && lane < pnfr) ob[NC * rowT + lane] = nyv;
-        }
-        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-      }
-      STAMP(4);
-      LDS_BARRIER();  // B
-      STAMP(5);
-      if (!have) break;
-      pb = clip_of(u);
-      pf0 = frame0_of(u);
-      pnfr = min(FPB, T - pf0);
-    }
-    return;
-  }
-
-  // -------------------------------------------------------------------- compute waves
-  float wwe[16], wwo[16];
-  {
-    const int lane = threadIdx.x & 63;
-    double sn, cs;
-    sincospi((2.0 * lane) / 2048.0, &sn, &cs);
-    const c2 e1 = mk((float)cs, (float)-sn);
-    sincospi((2.0 * lane + 1.0) / 2048.0, &sn, &cs);
-    const c2 eh = mk((float)cs, (float)-sn);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      wwe[j] = hann_sq(e1, j);
-      wwo[j] = hann_sq(eh, j);
-    }
-  }
-  c2* S = scratch + wave * SCR;
-  const int fl = wave;
-  LDS_BARRIER();  // prologue barrier
-#pragma unroll 1
-  for (int u = wi, it = 0;; u += W, ++it) {
-    int tid = threadIdx.x, toff = 0;
-    __asm__ volatile("" : "+v"(tid), "+v"(toff));
-    const FftTabs& tbl = *reinterpret_cast<const FftTabs*>(reinterpret_cast<const char*>(&tb) + toff);
-    const int lane = tid & 63;
-    if (u >= U) {  // the memory waves' last write-out pass
-      LDS_BARRIER();
-      LDS_BARRIER();
-      break;
-    }
-    float2 raw[16];
-    STAMP(0);
-    {
-      const float2* src = reinterpret_cast<const float2*>(span + fl * hop) + lane;  // hop even
-#pragma unroll
-      for (int j = 0; j < 16; ++j) raw[j] = src[64 * j];
-    }
-    LDS_BARRIER();  // A: SP read out (lgkmcnt(0) first)
-    STAMP(1);
-    const int f0 = frame0_of(u);
-    const int nfr = min(FPB, T - f0);
-    float* Sf = st[it & 1];
-    if (fl < nfr) {
-      c2 v[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) v[j] = mk(raw[j].x * wwe[j], raw[j].y * wwo[j]);
-      STAMP(2);
-      fft1024_v2(v, S, tbl, lane);
-      STAMP(3);
-      if (!MELM) {
-        float res[17];
-        power_pairs_v2<MODE == MODE_LOGPOW>(v, tbl, lane, res);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          Sf[stage_pos<FPB>(fl, lane + 64 * j)] = res[2 * j];
-          if (lane + j > 0) Sf[stage_pos<FPB>(fl, NC - lane - 64 * j)] = res[2 * j + 1];
-        }
-        if (lane == 0) {
-          Sf[stage_pos<FPB>(fl, NC / 2)] = res[16];
-          ny[it & 1][fl] = res[1];
-        }
-        STAMP(4);
-      } else {
-        float r[17];
-        power_pairs_v2<false>(v, tbl, lane, r);
-        float* P = reinterpret_cast<float*>(S);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          P[lane + 64 * j] = r[2 * j];
-          P[NC - lane - 64 * j] = r[2 * j + 1];
-        }
-        if (lane == 0) P[NC / 2] = r[16];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-          const int m = lane + 64 * qq;
-          float acc = 0.f;
-          if (m < mel.n_mels) {
-            const int s0 = mel.start[m], n = mel.len[m], wo2 = mel.woff[m];
-            float a1 = 0.f, a2 = 0.f, a3 = 0.f;
-            const float* wq = mel.w + wo2;
-            const float* pq = P + s0;
-            int i = 0;
-            for (; i + 4 <= n; i += 4) {
-              acc += wq[i] * pq[i];
-              a1 += wq[i + 1] * pq[i + 1];
-              a2 += wq[i + 2] * pq[i + 2];
-              a3 += wq[i + 3] * pq[i + 3];
-            }
-            for (; i < n; ++i) acc += wq[i] * pq[i];
-            acc = (acc + a1) + (a2 + a3);
-          }
-          Sf[fl * RSTR_MEL + m] = acc;
-        }
-      }
-    }
-    LDS_BARRIER();  // B
-    STAMP(5);
-  }
-}
-
-#undef STAMP
-#undef LDS_BARRIER
-
 // ---------------------------------------------------------------------------
 // iSTFT (librosa.istft, center=True, Hann): workgroup = 512 threads, output segment of
 // SEG = 16 samples per thread. Frames overlapping the segment are inverse-FFT'd 8 at a
@@ -1823,54 +1594,18 @@ __global__ void transpose_mag_kernel(const float* __restrict__ S, int F, int T, 
   }
 }
 
-static bool stft_cx_fm() {  // MST_STFT_CX_FM=0: complex STFT on the round-1 kernel (A/B)
-  static const bool v = [] {
-    const char* e = getenv("MST_STFT_CX_FM");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-static bool stft_ws() {  // MST_STFT_WS=1: the warp-specialised kernel (A/B; no faster, see DESIGN)
-  static const bool v = [] {
-    const char* e = getenv("MST_STFT_WS");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 int stft_launch(int mode, const float* x, int B, int L, int n_fft, int hop, int pad_mode, float* out,
                 MelTab mel, hipStream_t st) {
   MST_REQUIRE(x && out && B > 0 && n_fft == NFFT && hop > 0);
   MST_REQUIRE(L > NFFT / 2 || pad_mode == MST_PAD_CONSTANT);
   MST_REQUIRE(pad_mode == MST_PAD_REFLECT || pad_mode == MST_PAD_CONSTANT);
   const int T = 1 + L / hop;
-  if (mode != MODE_COMPLEX && !(hop & 1) && hop <= 256 && stft_ws()) {
-    // warp-specialised: one 768-thread workgroup per CU (32 per XCD group)
-    const long long per_group = (long long)ceil_div(B, 8) * ceil_div(T, WS_CW);
-    const int W = (int)(per_group < 32 ? per_group : 32);
-    dim3 grid(8 * W), block(64 * (WS_CW + WS_MW));
-    const long long rows = mode == MODE_MEL ? mel.n_mels : NB;
-    MST_REQUIRE(rows * T * 4 < (1ll << 31));  // per-clip buffer descriptors
-    MST_REQUIRE(mode != MODE_MEL || mel.n_mels <= 128);
-    const bool v4 = (T & 3) == 0 && ((uintptr_t)out & 15) == 0;
-#define MST_STFT_WS(M) do { if (v4) hipLaunchKernelGGL((stft_ws_kernel<M, true>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W); \
-                            else hipLaunchKernelGGL((stft_ws_kernel<M, false>), grid, block, 0, st, x, B, L, T, hop, pad_mode, out, mel, W); } while (0)
-    switch (mode) {
-      case MODE_LOGPOW: MST_STFT_WS(MODE_LOGPOW); break;
-      case MODE_POWER: MST_STFT_WS(MODE_POWER); break;
-      default: MST_STFT_WS(MODE_MEL); break;
-    }
-#undef MST_STFT_WS
-    MST_CHECK_LAUNCH();
-    return MST_OK;
-  }
   // frames per block: 16 (one 1024-thread workgroup per CU, 64-byte row pieces) for the
   // log-power / power STFT, 8 (two workgroups per CU) for mel and the complex STFT
   // (profiles/r03/ab_fm16.txt: log-power 0.166 -> 0.162 ms; mel +2 %, Griffin-Lim +8 % at 16)
   const int fmw = (mode == MODE_LOGPOW || mode == MODE_POWER) ? FM_WAVES_POW : FM_WAVES;
   const bool fm_fits = !(hop & 1) && (long long)((fmw - 1) * hop + NFFT) * 4 <= (long long)fmw * (SCR * 8 - NC * 4);
-  if (mode == MODE_COMPLEX && !(fm_fits && stft_cx_fm())) {  // frame-major (B, T, F, 2), round-1 kernel
+  if (mode == MODE_COMPLEX && !fm_fits) {  // frame-major (B, T, F, 2), round-1 kernel
     dim3 grid(ceil_div(T, FR), B), block(512);
     hipLaunchKernelGGL(stft_kernel<MODE_COMPLEX>, grid, block, 0, st, x, L, T, hop, pad_mode, out, mel);
   } else if (!fm_fits) {
@@ -1930,12 +1665,8 @@ int istft2_launch(const float2* cur, const float2* prev, const float* mag, float
 // One-pass Griffin-Lim synthesis (gl_synth_kernel). Seam samples (shared by two workgroups) are
 // added atomically into y, whose seams must be zero on entry; the launch zeroes the seams of
 // `ynext` (the next synthesis target) as it goes.
-static bool gl_one_pass(int hop) {
-  static const bool two = [] {  // MST_GL_TWO_PASS=1: the frames-workspace path (A/B tuning)
-    const char* e = getenv("MST_GL_TWO_PASS");
-    return e && e[0] == '1';
-  }();
-  return !two && hop <= 1024;
+static bool gl_one_pass(int hop) {  // hop > 1024: the two-pass frames-workspace path
+  return hop <= 1024;
 }
 
 int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, float beta,

@@ -1,4 +1,5 @@
-// Implicit-GEMM conv/linear kernels on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// Implicit-GEMM conv/linear kernels on gfx950: fp32 products on the bf16 matrix cores
+// (v_mfma_f32_32x32x16_bf16, operands split exactly into three bf16 planes, see below).
 //
 // One kernel body serves every dense contraction of PerformanceNet (model/model.py):
 //   forward  Conv1d k3 p1 (model.py:14-22), Linear (model.py:98-99, NCL = 1-tap conv),
@@ -13,11 +14,8 @@
 // gate (DenseConcat backward).
 //
 // Tile: 128x128 block, BK=32, 256 threads = 4 waves in 2x2, each wave 64x64 = 2x2
-// MFMA 32x32 tiles. LDS holds A as [m][k] and B as [n][k] (k contiguous, row stride
-// 36 floats => conflict-free ds_read_b128 / ds_write_b128), double buffered with
-// register-staged prefetch (global loads of tile k+1 in flight during tile k's MFMAs).
-// Lane half h = lane>>5 owns k in [16h, 16h+16) of each BK tile, so one ds_read_b128
-// gives a lane four consecutive MFMA k-steps.
+// MFMA 32x32 tiles. Global loads are register-staged two tiles ahead; each loaded element is
+// split once into three bf16 planes when it is stored to LDS (see pl_off).
 //
 // Operands are fetched with raw buffer loads (32-bit byte offsets into a descriptor per
 // tensor): an element outside the tensor's valid ranges gets an out-of-range offset and the
@@ -32,7 +30,7 @@
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256, LDK = BK + 4;
+constexpr int BM = 128, BN = 128, BK = 32, NTHR = 256;
 
 constexpr uint32_t OOB = 0x7FFFFFF0u;  // byte offset past every descriptor's num_records
 constexpr int MAXCLS = 8;              // wgrad K classes
@@ -47,41 +45,17 @@ typedef __amdgpu_buffer_rsrc_t rsrc_t;
 // product is exact and v_mfma_f32_32x32x16_bf16 accumulates in fp32, so the result carries
 // fp32-level error (tests/test_gpu_kernels.py bounds it with the fp32 tolerances) at 6 MFMAs
 // of 32 cycles per 16-deep k step instead of 8 fp32 MFMAs of 64 cycles: 2.7x less matrix-
-// core time. MST_GEMM_X6=0 builds the fp32-MFMA inner loop instead; MST_GEMM_X6=1 keeps fp32
-// tiles in LDS and splits after every LDS read (each element split by both waves reading it).
-#ifndef MST_GEMM_X6
-#define MST_GEMM_X6 2  // 2: split once at the LDS store (default); 1: split after each LDS read
-#endif
+// core time. (Rounds 1-2 ran v_mfma_f32_32x32x2_f32 on fp32 tiles and then split after every
+// LDS read; both were measured slower and removed: DESIGN.md, GEMM design.)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 struct Split3 {
   bf16x8 h, m, l;
 };
 
-// 8 consecutive fp32 (two 16-byte LDS reads) -> three bf16 planes
-__device__ __forceinline__ Split3 split3(const float* q) {
-  const f32x4 u = *reinterpret_cast<const f32x4*>(q);
-  const f32x4 w = *reinterpret_cast<const f32x4*>(q + 4);
-  Split3 s;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const float x = i < 4 ? u[i] : w[i - 4];
-    const __bf16 b0 = (__bf16)x;
-    const float r1 = x - (float)b0;
-    const __bf16 b1 = (__bf16)r1;
-    const float r2 = r1 - (float)b1;
-    s.h[i] = b0;
-    s.m[i] = b1;
-    s.l[i] = (__bf16)r2;
-  }
-  return s;
-}
-
-// MST_GEMM_X6 == 2 (default): the split happens once per element, when a loaded tile is stored:
-// A and B sit in LDS as three bf16 planes (hi, mid, lo) of [row][k] with 40-element rows (80 B:
-// the 16-byte fragment reads of 16 consecutive rows hit disjoint bank quads). The 6 planes
-// (60 KB) take ONE buffer (the 64 KB epilogue tile aliases it), so two workgroups still fit per
-// CU: the tile loop stores, syncs, runs the MFMAs, syncs, and the other workgroup on the CU
-// fills the store phase. Each element is split once instead of by both waves that read it.
+// The split happens once per element, when a loaded tile is stored: A and B sit in LDS as
+// three bf16 planes (hi, mid, lo) of [row][k]. The 6 planes (48 KB) take ONE buffer (the 64 KB
+// epilogue tile aliases it), so two workgroups fit per CU: the tile loop stores, syncs, runs the
+// MFMAs, syncs, and the other workgroup on the CU fills the store phase.
 // Plane rows are 64 B (32 bf16, no padding) with the four 16-byte quads of row r XOR-swizzled by
 // (r >> 2) & 3: a 16-row fragment read (16-byte lanes) and a 4-row k-major write (8-byte lanes,
 // 8 per row) each cover every bank once, and the row-major writes pair two k quads into one
@@ -146,76 +120,11 @@ __device__ __forceinline__ Split3 ld_planes(const __bf16* base, int row, int q) 
   return s;
 }
 
-// MST_GEMM_X6 == 3: the same bf16 planes, but LDS holds two HALF tiles (16-deep k, 24 KB each,
-// 48 KB with the 64 KB epilogue tile aliasing them): while a wave runs the MFMAs of one half it
-// splits and stores the next half into the other buffer, so the split VALU and the LDS writes
-// sit between its MFMAs instead of in a store phase of their own, and each workgroup barrier
-// ends a phase that holds both. Plane rows are 32 B (two 16-byte quads, swapped when bit 3 of
-// the row is set: the 16-row fragment reads cover all 64 banks). Loader units are laid out so
-// that every thread holds data of both halves (see km_r / km_q / rm_quad).
-constexpr int PLANE_H = BM * 16;  // bf16 elements per half-tile plane
-__device__ __forceinline__ int plh_off(int row, int q) {  // element offset of (row, 16-B quad q)
-  return row * 16 + 8 * (q ^ ((row >> 3) & 1));
-}
-__device__ __forceinline__ void split_store4h(__bf16* plane0, int row, int c, const f32x4 v) {
-  bf16x4 hi, mid, lo;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const Bf3 t = split1(v[i]);
-    hi[i] = t.h;
-    mid[i] = t.m;
-    lo[i] = t.l;
-  }
-  const int off = plh_off(row, c >> 1) + 4 * (c & 1);
-  *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
-  *reinterpret_cast<bf16x4*>(plane0 + PLANE_H + off) = mid;
-  *reinterpret_cast<bf16x4*>(plane0 + 2 * PLANE_H + off) = lo;
-}
-__device__ __forceinline__ void split_store8h(__bf16* plane0, int row, int q, const f32x4 v0,
-                                              const f32x4 v1) {
-  bf16x8 hi, mid, lo;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const Bf3 t = split1(i < 4 ? v0[i] : v1[i - 4]);
-    hi[i] = t.h;
-    mid[i] = t.m;
-    lo[i] = t.l;
-  }
-  const int off = plh_off(row, q);
-  *reinterpret_cast<bf16x8*>(plane0 + off) = hi;
-  *reinterpret_cast<bf16x8*>(plane0 + PLANE_H + off) = mid;
-  *reinterpret_cast<bf16x8*>(plane0 + 2 * PLANE_H + off) = lo;
-}
-__device__ __forceinline__ Split3 ld_planes_h(const __bf16* base, int row, int q) {
-  const __bf16* p = base + plh_off(row, q);
-  Split3 s;
-  s.h = *reinterpret_cast<const bf16x8*>(p);
-  s.m = *reinterpret_cast<const bf16x8*>(p + PLANE_H);
-  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PLANE_H);
-  return s;
-}
+// Row-major tile units: thread (row, kw) holds 4-float k units rm_quad(kw, u) = 4 kw + u,
+// u = 0..3 (a thread's units adjacent, stored to the planes in pairs).
+__device__ __forceinline__ constexpr int rm_quad(int kw, int u) { return 4 * kw + u; }
 
-// Row-major tile units: thread (row, kw) holds 4-float k units rm_quad(kw, u), u = 0..3. The
-// bf16-plane path takes 4 kw + u (a thread's units adjacent, stored in pairs); the half-tile path
-// 2 kw + (u & 1) + 4 (u >> 1) (units 0, 1 in the first 16-deep half, 2, 3 in the second, each
-// pair adjacent); the fp32 path kw + 2 u.
-__device__ __forceinline__ constexpr int rm_quad(int kw, int u) {
-  return MST_GEMM_X6 == 3 ? 2 * kw + (u & 1) + 4 * (u >> 1) : (MST_GEMM_X6 == 2 ? 4 * kw + u : kw + 2 * u);
-}
-
-// MST_GEMM_OCC: resident workgroups per CU. 2 (default): 64 KB of LDS (the epilogue tile) and two
-// register stages. 3 (build-time A/B): the 48 KB of planes only (the epilogue goes through LDS in
-// two 64-row halves), one register stage (tile k+1 loads while tile k's MFMAs run), <= 168 VGPRs.
-#ifndef MST_GEMM_OCC
-#define MST_GEMM_OCC 2
-#endif
-static_assert(MST_GEMM_OCC == 2 || (MST_GEMM_OCC == 3 && MST_GEMM_X6 == 2), "3 workgroups per CU: bf16-plane build only");
-// occupancy per kernel kind: the weight-gradient kernels keep 2 (their per-class element offsets
-// do not fit 168 VGPRs)
-__host__ __device__ constexpr int occ_of(bool wg) { return (MST_GEMM_OCC == 3 && !wg) ? 3 : 2; }
-constexpr int LDS_NBUF = MST_GEMM_X6 >= 2 ? 1 : 2;
-constexpr int LDS_FLOATS = MST_GEMM_X6 >= 2 ? BM * BN : (BM + BN) * LDK;  // floats per buffer
-__host__ __device__ constexpr int lds_floats(bool wg) { return occ_of(wg) == 3 ? 3 * PLANE : LDS_FLOATS; }
+constexpr int LDS_FLOATS = BM * BN;  // the 64 KB epilogue tile; the 48 KB of planes alias it
 
 // acc += a . b over one 16-deep k step, smallest products first
 __device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
@@ -385,8 +294,8 @@ __device__ __forceinline__ f32x4 ldbs4(rsrc_t r, uint32_t voff, int soff) {
 
 // One pass over K tiles [kt0, kt1) of output tile (m_t, n_t), then the epilogue: the final
 // values (direct), split-K slab `split`, or (slab != nullptr) a stream-K partial tile.
-template <int TAPS, bool WG, int AMODE, bool DUAL, int LF = LDS_FLOATS>
-__device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t,
+template <int TAPS, bool WG, int AMODE, bool DUAL>
+__device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
                                           int n_t, int kt0, int kt1, int split, float* slab,
                                           int tid) {
   const int lane = tid & 63;
@@ -399,18 +308,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
   //   KM ("k-major"): row = (tid>>3) + 32u, k quad = tid&7 -> 8 lanes run along k
   //   RM ("row-major"): row = tid&127, k quads rm_quad(kw, u) -> lanes run along rows; k is
   //                     wave-uniform (kw = tid>>7 via readfirstlane), so its decode is scalar
-  // fp32 path: both store a unit as one conflict-free ds_write_b128 into the [row][k] image;
-  // bf16-plane path: see pl_off.
+  // both are split into the bf16 planes at the LDS store (pl_off).
   // A: AMODE 1 (k-contiguous, float4) and 0 (k-scalar) use KM; AMODE 2 (m-contiguous) RM.
   // B: conv/dgrad (n = time, contiguous) RM; wgrad (k = time) KM.
-  // k-major unit u of this thread: row km_r(u), 4-float k unit km_q(u) (8 lanes along k per row;
-  // half-tile path: 4 lanes per row, units 0, 2 in the first 16-deep half and 1, 3 in the second)
-  auto km_r = [&](int u) __attribute__((always_inline)) {
-    return MST_GEMM_X6 == 3 ? (tid >> 2) + 64 * (u >> 1) : (tid >> 3) + 32 * u;
-  };
-  auto km_q = [&](int u) __attribute__((always_inline)) {
-    return MST_GEMM_X6 == 3 ? (tid & 3) + 4 * (u & 1) : (tid & 7);
-  };
+  // k-major unit u of this thread: row km_r(u), 4-float k unit km_q(u) (8 lanes along k per row)
+  auto km_r = [&](int u) __attribute__((always_inline)) { return (tid >> 3) + 32 * u; };
+  auto km_q = [&](int u) __attribute__((always_inline)) { return tid & 7; };
   const int rm_row = tid & 127;
   const int kw = __builtin_amdgcn_readfirstlane(tid >> 7);
 
@@ -538,35 +441,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
     }
   };
 
-  // half-tile path: store 16-deep half h of register stage S into LDS half-buffer hb
-  auto store_half = [&](auto S, int h, int hb) __attribute__((always_inline)) {
+  auto store_tile = [&](auto S) __attribute__((always_inline)) {
     constexpr int st = decltype(S)::value;
-    __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]) + hb * 6 * PLANE_H;
-    __bf16* Bp = Ap + 3 * PLANE_H;
-    if constexpr (AMODE == 2 && !WG) {
-      split_store8h(Ap, rm_row, kw, ra[st][2 * h], ra[st][2 * h + 1]);
-    } else {
-      split_store4h(Ap, km_r(h), tid & 3, ra[st][h]);
-      split_store4h(Ap, km_r(h + 2), tid & 3, ra[st][h + 2]);
-    }
-    if constexpr (WG) {
-      split_store4h(Bp, km_r(h), tid & 3, rb[st][h]);
-      split_store4h(Bp, km_r(h + 2), tid & 3, rb[st][h + 2]);
-    } else {
-      split_store8h(Bp, rm_row, kw, rb[st][2 * h], rb[st][2 * h + 1]);
-    }
-  };
-  (void)store_half;
-
-  auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
-    constexpr int st = decltype(S)::value;
-#if MST_GEMM_X6 == 3
-    (void)buf;
-    (void)st;
-    return;
-#elif MST_GEMM_X6 == 2
-    (void)buf;
-    __bf16* Ap = reinterpret_cast<__bf16*>(lds[0]);
+    __bf16* Ap = reinterpret_cast<__bf16*>(lds);
     __bf16* Bp = Ap + 3 * PLANE;
     if constexpr (AMODE == 2 && !WG) {  // quads 4 kw + u: pairs (0, 1), (2, 3) are adjacent
 #pragma unroll
@@ -581,26 +458,6 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
     } else {
 #pragma unroll
       for (int u = 0; u < 4; u += 2) split_store8(Bp, rm_row, 2 * kw + u / 2, rb[st][u], rb[st][u + 1]);
-    }
-    return;
-#endif
-    float* As = lds[buf];
-    float* Bs = lds[buf] + BM * LDK;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 v = ra[st][u];
-      if constexpr (AMODE == 2 && !WG)
-        *reinterpret_cast<f32x4*>(As + rm_row * LDK + rm_quad(kw, u) * 4) = v;
-      else
-        *reinterpret_cast<f32x4*>(As + km_r(u) * LDK + 4 * km_q(u)) = v;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 v = rb[st][u];
-      if constexpr (WG)
-        *reinterpret_cast<f32x4*>(Bs + km_r(u) * LDK + 4 * km_q(u)) = v;
-      else
-        *reinterpret_cast<f32x4*>(Bs + rm_row * LDK + rm_quad(kw, u) * 4) = v;
     }
   };
 
@@ -620,27 +477,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
   // vmcnt(0) between the prefetch and this tile's MFMAs.
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  // half-tile path: the 16-deep MFMA step of LDS half-buffer hb
-  auto mfma_half = [&](int hb) __attribute__((always_inline)) {
-    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]) + hb * 6 * PLANE_H;
-    const __bf16* Bp = Ap + 3 * PLANE_H;
-    const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
-    const Split3 a0 = ld_planes_h(Ap, ra0, h), a1 = ld_planes_h(Ap, ra0 + 32, h);
-    const Split3 b0 = ld_planes_h(Bp, rb0, h), b1 = ld_planes_h(Bp, rb0 + 32, h);
-    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
-    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
-    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
-    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
-  };
-  (void)mfma_half;
-
-  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-#if MST_GEMM_X6 == 3
-    (void)buf;
-#elif MST_GEMM_X6 == 2
+  auto mfma_tile = [&]() __attribute__((always_inline)) {
     // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
-    (void)buf;
-    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds[0]);
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds);
     const __bf16* Bp = Ap + 3 * PLANE;
     const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
 #pragma unroll
@@ -657,43 +496,13 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
         acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
       }
     }
-#elif MST_GEMM_X6
-    // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
-    const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 8;
-    const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 8;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const Split3 a0 = split3(As + 16 * s), a1 = split3(As + 32 * LDK + 16 * s);
-      const Split3 b0 = split3(Bs + 16 * s), b1 = split3(Bs + 32 * LDK + 16 * s);
-      acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
-      acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
-      acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
-      acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
-    }
-#else
-    const float* As = lds[buf] + (wm * 64 + r32) * LDK + h * 16;
-    const float* Bs = lds[buf] + BM * LDK + (wn * 64 + r32) * LDK + h * 16;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      f32x4 a0 = *reinterpret_cast<const f32x4*>(As + g * 4);
-      f32x4 a1 = *reinterpret_cast<const f32x4*>(As + 32 * LDK + g * 4);
-      f32x4 b0 = *reinterpret_cast<const f32x4*>(Bs + g * 4);
-      f32x4 b1 = *reinterpret_cast<const f32x4*>(Bs + 32 * LDK + g * 4);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
-      }
-    }
-#endif
   };
 
-  // Pipeline: LDS double buffer + two register stages. Iteration k issues the global loads of
-  // tile k+2, runs tile k's MFMAs from LDS, then stores tile k+1 (loaded one iteration
-  // earlier, so its latency is covered by a full tile of MFMAs) into the other LDS buffer.
-  // Loads past the end are harmless (bounded buffer loads) and never consumed.
+  // Pipeline: one LDS buffer of planes + two register stages. Iteration k issues the global
+  // loads of tile k+2, runs tile k's MFMAs from LDS, syncs, then splits and stores tile k+1
+  // (loaded one iteration earlier, so its latency is covered by a full tile of MFMAs); the other
+  // workgroup on the CU runs its MFMAs while this one stores. Loads past the end are harmless
+  // (bounded buffer loads) and never consumed.
   // run(): one pipelined pass over tiles [kb, ke) starting at scalar decode (tap, blk).
   //   conv : (tap, source block) of a tap-major K
   //   wgrad: (batch row b, tile index j within the class), `per` tiles per row
@@ -706,108 +515,36 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
     };
     load_tile(I0{}, kb, tap, blk);
     advance();
-    if constexpr (occ_of(WG) != 3) {
-      load_tile(I1{}, kb + 1, tap, blk);
-      advance();
-    }
-#if MST_GEMM_X6 == 3
-    store_half(I0{}, 0, 0);
-    __syncthreads();
-    // Per 32-deep tile kt (register stage sb; stage sb ^ 1 holds tile kt + 1, in flight):
-    //   phase A: MFMAs of kt's first half (buffer 0) | split + store kt's second half -> buffer 1
-    //   phase B: loads of tile kt + 2 into stage sb (free now) | MFMAs of kt's second half
-    //            (buffer 1) | split + store tile kt + 1's first half -> buffer 0
-    // Each phase ends in one barrier; a buffer is written only in the phase after the one that
-    // read it. VALU and LDS writes are placed between the MFMAs (sched_group_barrier).
-    constexpr int NV3 = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
-    auto step = [&](auto S, int kt) __attribute__((always_inline)) {
-      constexpr int sb = decltype(S)::value;
-      mfma_half(0);
-      store_half(S, 1, 1);
-      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);  // the step's fragment reads
-#pragma unroll
-      for (int i = 0; i < 24; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);  // VALU (split)
-        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-      }
-      __syncthreads();
-      load_tile(S, kt + 2, tap, blk);
-      advance();
-      mfma_half(1);
-      store_half(std::integral_constant<int, sb ^ 1>{}, 0, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-      for (int i = 0; i < 24; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (i < NV3) __builtin_amdgcn_sched_group_barrier(0x020, NV3 > 24 ? 2 : 1, 0);  // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
-        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-      }
-      __syncthreads();
-    };
-    for (int kt = kb; kt < ke; kt += 2) {
-      step(I0{}, kt);
-      if (kt + 1 < ke) step(I1{}, kt + 1);
-    }
-#else
-    if constexpr (occ_of(WG) == 3) {
-    // one register stage: tile kt + 1 loads during tile kt's MFMAs and is stored after them
-    store_tile(I0{}, 0);
-    __syncthreads();
-    auto step = [&](auto S, int kt) __attribute__((always_inline)) {
-      (void)S;
-      load_tile(I0{}, kt + 1, tap, blk);
-      advance();
-      mfma_tile(0);
-      constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
-      constexpr int PER = 48 / NV > 2 ? 2 : (48 / NV < 1 ? 1 : 48 / NV);
-#pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
-      }
-      __syncthreads();
-      store_tile(I0{}, 0);
-      __syncthreads();
-    };
-    for (int kt = kb; kt < ke; kt += 2) {
-      step(I0{}, kt);
-      if (kt + 1 < ke) step(I1{}, kt + 1);
-    }
-    } else {
-    store_tile(I0{}, 0);
+    load_tile(I1{}, kb + 1, tap, blk);
+    advance();
+    store_tile(I0{});
     __syncthreads();
     auto step = [&](auto S, int kt) __attribute__((always_inline)) {
       constexpr int sb = decltype(S)::value;
       load_tile(S, kt + 2, tap, blk);
       advance();
-      mfma_tile(sb);
+      mfma_tile();
       // Interleave the next-tile global loads with this tile's MFMAs, one load per two MFMAs
       // (sched_group_barrier). Issued as a block above the MFMAs they cost 15-25 % of the
       // GEMM (A/B: conv fwd +5-10 %, dgrad +9-13 %, wgrad +15-25 %); left to the scheduler
       // they sink next to their wait.
       constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
-      constexpr int NMF = MST_GEMM_X6 ? 48 : 64;                 // MFMAs per tile per wave
+      constexpr int NMF = 48;                                    // MFMAs per tile per wave
       constexpr int PER = NMF / NV > 2 ? 2 : (NMF / NV < 1 ? 1 : NMF / NV);
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
         __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
       }
-      if constexpr (MST_GEMM_X6 == 2) __syncthreads();  // one buffer: its MFMA reads first
-      store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);
+      __syncthreads();  // one buffer: its MFMA reads first
+      store_tile(std::integral_constant<int, sb ^ 1>{});
       __syncthreads();
     };
     for (int kt = kb; kt < ke; kt += 2) {
       step(I0{}, kt);
       if (kt + 1 < ke) step(I1{}, kt + 1);
     }
-    }
-#endif
   };
-  (void)store_tile;
-  (void)mfma_tile;
   if constexpr (!WG) {
     if (kt0 < kt1) {
       const int tap = kt0 / p.nbT;
@@ -827,10 +564,8 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
     }
   }
 
-  // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores (EPI_ROWS rows per pass;
-  // with two passes the waves of row half wm write in pass wm) ----
-  constexpr int EPI_ROWS = LF >= BM * BN ? BM : BM / 2;
-  float* Cs = &lds[0][0];  // EPI_ROWS x 128 floats: the A/B buffers' space
+  // ---- epilogue: accumulators -> LDS tile -> row-contiguous stores ----
+  float* Cs = lds;  // BM x BN floats: the planes' space
   const int nl = tid & (BN - 1);
   const int n = n0 + nl;
   // the tile's bias values, staged once in LDS (read back as broadcasts: a wave's row is
@@ -838,41 +573,35 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
   __shared__ float s_bias[BM];
   const bool use_bias = !WG && !slab && p.splitk <= 1 && p.bias != nullptr;
   if (use_bias && tid < BM) s_bias[tid] = m0 + tid < p.M ? p.bias[m0 + tid] : 0.f;
+  __syncthreads();
 #pragma unroll
-  for (int ep = 0; ep < BM / EPI_ROWS; ++ep) {
-    __syncthreads();
-    if (EPI_ROWS == BM || wm == ep) {
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int ml = (EPI_ROWS == BM ? wm * 64 : 0) + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int nl2 = wn * 64 + j * 32 + r32;
-            Cs[ml * BN + nl2] = acc[i][j][r];
-          }
-    }
-    __syncthreads();
-    if (n < p.N) {
-      for (int mr = tid >> 7; mr < EPI_ROWS; mr += NTHR / BN) {
-        const int ml = ep * EPI_ROWS + mr;
-        const int m = m0 + ml;
-        if (m >= p.M) break;
-        const float v = Cs[mr * BN + nl];
-        if (slab) {
-          slab[ml * BN + nl] = v;
-        } else if (p.splitk > 1) {
-          p.ws[((long long)split * p.M + m) * p.N + n] = v;
-        } else if constexpr (WG) {
-          wgrad_store(p, m, n, v);
-        } else {
-          conv_store_b(p, m, n, v, use_bias ? s_bias[ml] : 0.f);
-        }
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl2 = wn * 64 + j * 32 + r32;
+        Cs[ml * BN + nl2] = acc[i][j][r];
+      }
+  __syncthreads();
+  if (n < p.N) {
+    for (int ml = tid >> 7; ml < BM; ml += NTHR / BN) {
+      const int m = m0 + ml;
+      if (m >= p.M) break;
+      const float v = Cs[ml * BN + nl];
+      if (slab) {
+        slab[ml * BN + nl] = v;
+      } else if (p.splitk > 1) {
+        p.ws[((long long)split * p.M + m) * p.N + n] = v;
+      } else if constexpr (WG) {
+        wgrad_store(p, m, n, v);
+      } else {
+        conv_store_b(p, m, n, v, use_bias ? s_bias[ml] : 0.f);
       }
     }
   }
-  __syncthreads();  // Cs aliases the A/B buffers the next pass starts writing
+  __syncthreads();  // Cs aliases the planes the next pass (stream-K) starts writing
 }
 
 // Schedules. Data-parallel / split-K: one (tile, split) per workgroup, grid (nx, ny, splitk).
@@ -883,12 +612,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float (*lds)[LF], int m_t
 // 2v + 1 (its last), which sk_fixup_kernel sums in workgroup order. Every workgroup then does
 // the same work, so there is no partial last wave.
 template <int TAPS, bool WG, int AMODE, bool DUAL>
-__global__ __launch_bounds__(NTHR, occ_of(WG)) void gemm_kernel(const GP p) {
-  constexpr int LF = lds_floats(WG);
-  static_assert(LDS_NBUF * LF >= BM * BN / 2, "epilogue half tile must fit the A/B buffers");
-  static_assert(MST_GEMM_X6 != 2 || 3 * PLANE <= LF, "bf16 planes must fit");
-  static_assert(MST_GEMM_X6 != 3 || 6 * PLANE_H <= LF, "two half-tile plane sets must fit");
-  __shared__ __attribute__((aligned(16))) float lds[LDS_NBUF][LF];
+__global__ __launch_bounds__(NTHR, 2) void gemm_kernel(const GP p) {
+  static_assert(6 * PLANE * 2 <= LDS_FLOATS * 4, "bf16 planes must fit the epilogue tile");
+  __shared__ __attribute__((aligned(16))) float lds[LDS_FLOATS];
   const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
   if (p.sk_L == 0) {
     const int W = nx * ny * (int)gridDim.z;
@@ -898,7 +624,7 @@ __global__ __launch_bounds__(NTHR, occ_of(WG)) void gemm_kernel(const GP p) {
     tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
     const int kt0 = (int)((long long)split * p.nk / p.splitk);
     const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
-    tile_pass<TAPS, WG, AMODE, DUAL, LF>(p, lds, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x);
     return;
   }
   const int v = xcd_order(blockIdx.x, gridDim.x);
@@ -913,81 +639,10 @@ __global__ __launch_bounds__(NTHR, occ_of(WG)) void gemm_kernel(const GP p) {
     tile_of(t, nx, ny, m_t, n_t);
     float* slab = (kt0 == 0 && kt1 == p.nk) ? nullptr
                                             : p.ws + (long long)(2 * v + slot) * (BM * BN);
-    tile_pass<TAPS, WG, AMODE, DUAL, LF>(p, lds, m_t, n_t, kt0, kt1, 0, slab, threadIdx.x);
+    tile_pass<TAPS, WG, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, 0, slab, threadIdx.x);
     it += kt1 - kt0;
     slot = 1;
   }
-}
-
-// __syncthreads() calls of one tile_pass over K tiles [kt0, kt1): one per pipelined run (its
-// prologue), two per K tile, three in the epilogue.
-template <bool WG>
-__device__ __forceinline__ int pass_barriers(const GP& p, int kt0, int kt1) {
-  static_assert(MST_GEMM_X6 >= 2, "two barriers per K tile");
-  int n = 3;
-  if constexpr (!WG) {
-    if (kt0 < kt1) n += 1 + 2 * (kt1 - kt0);
-  } else {
-    for (int c = 0; c < p.ncls; ++c) {
-      const int kb = max(kt0, p.cstart[c]), ke = min(kt1, p.cstart[c + 1]);
-      if (kb < ke) n += 1 + 2 * (ke - kb);
-    }
-  }
-  return n;
-}
-
-// Ping-pong schedule (round 3, default for split-K / data-parallel grids): one 512-thread
-// workgroup per CU holds two 256-thread groups, each running tile_pass on its own (tile, split)
-// with its own 64 KB LDS region, exactly as two 256-thread workgroups would. The difference is
-// that tile_pass's __syncthreads() now spans both groups, and group 1 enters one barrier later
-// than group 0: while group 0 runs a K tile's MFMAs, group 1 splits and stores its next tile into
-// LDS, and the other way round, on every SIMD (each holds one wave of each group). Two
-// independent workgroups drift into running the same phase at once (both MFMA, then both VALU);
-// here the barrier enforces the alternation. Both groups execute the same barrier sequence (same
-// GEMM, same K range length); an odd last virtual workgroup runs a tile of rows past M (all
-// loads out of range, no stores).
-template <int TAPS, bool WG, int AMODE, bool DUAL>
-__global__ __launch_bounds__(2 * NTHR, 1) void gemm_pp_kernel(const GP p) {
-  __shared__ __attribute__((aligned(16))) float lds[2][LDS_FLOATS];
-  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
-  const int g = threadIdx.x >> 8;
-  const int Wv = nx * ny * p.splitk;           // virtual (256-thread) workgroups
-  const int Wr = (Wv + 1) >> 1;                // real workgroups = gridDim.x
-  const int vw = 2 * xcd_order(blockIdx.x, Wr) + g;
-  int m_t, n_t, split = 0, kt0 = 0, kt1 = p.nk;
-  if (vw < Wv) {
-    split = vw / (nx * ny);
-    tile_of(vw - split * nx * ny, nx, ny, m_t, n_t);
-    kt0 = (int)((long long)split * p.nk / p.splitk);
-    kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
-  } else {  // the partner of an odd last group: same K range length as split 0, rows past M
-    m_t = ny;
-    n_t = 0;
-    kt1 = (int)((long long)p.nk / p.splitk);
-  }
-  // barrier counts of this group's pass and of its partner's: the shorter one pads at the end
-  // (K ranges of two splits can differ by a tile, and a weight-gradient range can cross a
-  // different number of K classes)
-  int pk0 = 0, pk1 = (int)((long long)p.nk / p.splitk);
-  const int pv = vw ^ 1;
-  if (pv < Wv) {
-    const int ps = pv / (nx * ny);
-    pk0 = (int)((long long)ps * p.nk / p.splitk);
-    pk1 = (int)((long long)(ps + 1) * p.nk / p.splitk);
-  }
-  const int mine = pass_barriers<WG>(p, kt0, kt1) + 1, theirs = pass_barriers<WG>(p, pk0, pk1) + 1;
-  if (g == 1) __syncthreads();  // enter one phase behind group 0
-  tile_pass<TAPS, WG, AMODE, DUAL>(p, lds + g, m_t, n_t, kt0, kt1, split, nullptr, threadIdx.x & (NTHR - 1));
-  if (g == 0) __syncthreads();  // ... and leave with the same barrier count
-  for (int i = mine; i < theirs; ++i) __syncthreads();
-}
-
-static bool gemm_pp() {  // MST_GEMM_PP=1: the ping-pong kernel (A/B; measured slower, see DESIGN)
-  static const bool v = [] {
-    const char* e = getenv("MST_GEMM_PP");
-    return e && e[0] == '1';
-  }();
-  return v;
 }
 
 // Stream-K fixup: one workgroup per (tile, quarter of its rows). A tile finished in place
@@ -1126,7 +781,7 @@ constexpr int SK_G = 512;
 // GEMMs' HBM-side traffic from 254 to 322 MB per launch (profiles/r01/gemm_traffic_m14_*.json):
 // a workgroup walking several tiles in sequence shares fewer panels through L2 with the
 // workgroups running beside it than one tile per workgroup does.
-void choose_sched(GP& p, int req, bool wg) {
+void choose_sched(GP& p, int req) {
   p.sk_L = p.sk_I = 0;
   const long long tiles = (long long)ceil_div(p.M, BM) * ceil_div(p.N, BN);
   int G = 0;
@@ -1144,7 +799,7 @@ void choose_sched(GP& p, int req, bool wg) {
     p.sk_I = tiles * p.nk;
     p.sk_L = (p.sk_I + G - 1) / G;
   } else {
-    p.splitk = choose_splitk(p.M, p.N, p.nk, req, occ_of(wg));
+    p.splitk = choose_splitk(p.M, p.N, p.nk, req, 2);
   }
 }
 
@@ -1171,15 +826,8 @@ int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   if (p.sk_L > 0) grid = dim3((unsigned)((p.sk_I + p.sk_L - 1) / p.sk_L), 1, 1);
   dim3 block(NTHR);
-  const bool pp = p.sk_L == 0 && gemm_pp();
-  const dim3 pgrid((unsigned)((grid.x * grid.y * grid.z + 1) / 2)), pblock(2 * NTHR);
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
-  if (pp) {                                                                          \
-    if (!WG && p.dual)                                                               \
-      hipLaunchKernelGGL((gemm_pp_kernel<TP, WG, AM, !WG>), pgrid, pblock, 0, st, p); \
-    else                                                                             \
-      hipLaunchKernelGGL((gemm_pp_kernel<TP, WG, AM, false>), pgrid, pblock, 0, st, p); \
-  } else if (!WG && p.dual)                                                          \
+  if (!WG && p.dual)                                                                 \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, !WG>), grid, block, 0, st, p);       \
   else                                                                               \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, false>), grid, block, 0, st, p);
@@ -1310,7 +958,7 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.drop_p = d->drop_p;
   p.seed = d->seed;
   p.seed_dev = reinterpret_cast<const unsigned long long*>(d->seed_dev);
-  choose_sched(p, d->splitk, false);
+  choose_sched(p, d->splitk);
   return MST_OK;
 }
 
@@ -1387,7 +1035,7 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
-  choose_sched(p, d->splitk, true);
+  choose_sched(p, d->splitk);
   return MST_OK;
 }
 
@@ -1406,7 +1054,7 @@ int wgrad_sources(const mst_wgrad_desc* d, mst_src* srcs, float** outs) {
 
 extern "C" {
 
-int mst_gemm_products(void) { return MST_GEMM_X6 ? 6 : 1; }
+int mst_gemm_products(void) { return 6; }
 
 size_t mst_conv_fwd_workspace_size(const mst_conv_desc* d) {
   GP p;

@@ -114,11 +114,12 @@ def test_griffinlim_vs_oracle(cuda):
 
 
 @pytest.mark.parametrize("hop,T", [(256, 6), (256, 24), (256, 25), (256, 49), (64, 200),
-                                   (128, 97), (512, 30), (1024, 15), (768, 20)])
+                                   (128, 97), (512, 30), (1024, 15), (768, 20), (1536, 10)])
 def test_griffinlim_synthesis_hops(cuda, hop, T):
     """The one-pass synthesis (gl_synth_kernel: workgroups of G frames, seams between them)
     across hops and frame counts: one workgroup, a last workgroup of one frame, several seams,
-    hops that do not divide n_fft (no window-sum-square table)."""
+    hops that do not divide n_fft (no window-sum-square table). hop > 1024 runs the two-pass
+    synthesis (ifft_frames_kernel + ola_kernel) and the round-1 complex STFT (stft_kernel)."""
     from ml_music_style_transfer_amd import spectral
     x = _piano(hop * (T - 1), 16000, 30 + T)
     S = np.abs(SR.stft(x, hop=hop, out_dtype=None)).astype(np.float32)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of the config-2 front end (bench_aux frontend leg) between STFT kernel knobs, plus the
 # STFT/mel parity tests. Dev tool, run on the GPU box:
-#   tools/ab_frontend.sh OUTDIR [NAME=ENV ...]     e.g. ws= v2=MST_STFT_WS=0
+#   tools/ab_frontend.sh OUTDIR [NAME=ENV ...]     e.g. base= lib2=MST_LIB_PATH=variants/x/libmst_hip.so
 set -e -o pipefail
 OUT=${1:?outdir}; shift; mkdir -p "$OUT"
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A GEMM build variant (VAR=variants/<name>/libmst_hip.so, e.g. -DMST_GEMM_X6=3 or -DMST_GEMM_OCC=3)
+# A GEMM build variant (VAR=variants/<name>/libmst_hip.so, built with EXTRA=-D... or from another tree)
 # vs the in-tree build: parity tests on the variant, then micro + bench A/B (dev tool; via gpurun).
 set -e -o pipefail
 OUT=gpurun_out/${1:?tag}; mkdir -p "$OUT"
