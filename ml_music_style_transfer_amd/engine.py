@@ -51,7 +51,10 @@ class GradSink:
     input-gradient GEMMs and norm kernels of the main stream: a GEMM's trailing partial wave of
     workgroups no longer leaves the chip half idle. Tensors a side launch reads are recorded on
     the side stream (the caching allocator must not hand them out again before it is done), and
-    the main stream waits for the side stream before the block listeners run and at the end."""
+    the main stream waits for the side stream before the block listeners run and at the end.
+    `joined` is the event the main stream last waited on: it completes with the last side-stream
+    launch (the side stream may still carry the caching allocator's free markers behind it,
+    which are events, not work)."""
 
     def __init__(self, flat_grad_of=None, on_ready=None, side=None):
         self.flat_grad_of = flat_grad_of or (lambda p: None)
@@ -59,6 +62,7 @@ class GradSink:
         self.side = side
         self._side_pending = False
         self._pending = []
+        self.joined = None
 
     def target(self, p):
         self._pending.append(p)
@@ -85,7 +89,10 @@ class GradSink:
 
     def join(self):
         if self._side_pending:
-            torch.cuda.current_stream().wait_stream(self.side)
+            ev = torch.cuda.Event()
+            ev.record(self.side)
+            torch.cuda.current_stream().wait_event(ev)
+            self.joined = ev
             self._side_pending = False
 
     def block_done(self):
@@ -424,6 +431,7 @@ class PerformanceNetFunction(torch.autograd.Function):
             for h in hooks:
                 h.ready(params)
         sink = module._grad_sink(on_ready if hooks else None)
+        module.__dict__["_mst_last_sink"] = sink  # tests inspect its join event
         g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need)
         for h in hooks:
             h.launch_remaining()

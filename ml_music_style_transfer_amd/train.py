@@ -328,7 +328,10 @@ class BackwardAdam:
         """Join the side stream. True when this backward's update has been issued."""
         if not (self.active and self.launched):
             return False
-        torch.cuda.current_stream().wait_stream(self.stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        torch.cuda.current_stream().wait_event(ev)
+        self.joined = ev  # completes with this step's last bucket update
         self.active = self.launched = False
         self.updates += 1
         return True

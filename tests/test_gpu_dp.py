@@ -328,4 +328,5 @@ def test_bench_two_ranks_one_gpu(tmp_path):
     ar = ln["allreduce"]
     assert "error" not in ar, ar
     assert ar["bus_GBps"] > 0 and "exposed_comm_ms_per_step" in ar and ar["overlapped"] is True
-    assert ar["grad_bytes"] == 4 * 726_039_425
+    # the flat gradient buffer: 726,039,425 live parameters in 16-byte aligned slots
+    assert 4 * 726_039_425 <= ar["grad_bytes"] < 4 * 726_039_425 + 16 * 1000

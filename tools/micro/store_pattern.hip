@@ -46,6 +46,36 @@ __global__ __launch_bounds__(512) void runs(float* out, int group) {
   }
 }
 
+// Wave-autonomous pattern (no LDS staging): each wave of a W-wave workgroup owns 4 consecutive
+// frames and stores, per lane, one float4 (its 4 frames) for each of the 16 bins it holds
+// (k = l + 64 j and 1024 - l - 64 j, as the STFT's register layout), plus bin 512 / 1024 from
+// lane 0; the W waves cover 4 W consecutive frames, the clip's blocks stay on one XCD.
+template <int W>
+__global__ __launch_bounds__(64 * W) void wave4(float* out) {
+  const int FR = 4 * W;
+  const int nblk = (T + FR - 1) / FR;
+  const int g = blockIdx.x;
+  const int b = (g / (8 * nblk)) * 8 + (g % 8);
+  const int blk = (g / 8) % nblk;
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int f = blk * FR + 4 * wave;
+  if (f + 3 >= T) return;
+  float* ob = out + (long long)b * F * T + f;
+  typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k0 = lane + 64 * j, k1 = 1024 - lane - 64 * j;
+    *reinterpret_cast<f4*>(ob + (long long)k0 * T) = f4{(float)k0, 1.f, 2.f, 3.f};
+    if (k1 != k0 && k1 < 1024 && lane + j > 0)
+      *reinterpret_cast<f4*>(ob + (long long)k1 * T) = f4{(float)k1, 1.f, 2.f, 3.f};
+  }
+  if (lane == 0) {
+    *reinterpret_cast<f4*>(ob + 512ll * T) = f4{512.f, 1.f, 2.f, 3.f};
+    *reinterpret_cast<f4*>(ob + 1024ll * T) = f4{1024.f, 1.f, 2.f, 3.f};
+  }
+}
+
 int main() {
   float* d;
   const size_t n = (size_t)B * F * T;
@@ -75,5 +105,11 @@ int main() {
   RUNS(16, 0, false) RUNS(16, 1, false)
   RUNS(32, 0, false) RUNS(32, 1, false) RUNS(32, 1, true)
   RUNS(64, 0, false) RUNS(64, 1, false)
+#define WAVE4(W)                                                                        \
+  time("wave4 x" #W " waves", [&] {                                                     \
+    const int nblk = (T + 4 * W - 1) / (4 * W);                                         \
+    wave4<W><<<((B + 7) / 8) * 8 * nblk, 64 * W>>>(d);                                  \
+  });
+  WAVE4(4) WAVE4(8) WAVE4(16)
   return 0;
 }
