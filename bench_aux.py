@@ -338,6 +338,9 @@ def griffinlim(args, world, rank, dev):
                         B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, extra)]
 
 
+MSS_SILENT_TOL = 2e-3  # targets with exact silence (see mss())
+
+
 def _torch_fp32_mss_gap(p, t, sizes, ref):
     """Relative gap of torch's fp32 CPU multi-scale loss (torch.stft) to the float64 oracle."""
     pt, qt, tot = torch.tensor(p), torch.tensor(t), 0.0
@@ -387,21 +390,29 @@ def mss(args, world, rank, dev):
         ref, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
                                                   tgt[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
         rel = abs(l0.item() - ref) / abs(ref)
-        # the piano target has exact silence (11 % of pair 0's samples) and bins far below fp32
-        # resolution, which log(S + 1e-7) amplifies: torch's own fp32 path misses float64 by
-        # ~1e-3 here, so the bar is max(1e-4, 1.5 x that gap) (tests/test_gpu_spectral.py)
+        # Fixed bars per input class. The piano target of pair 0 has exact silence (11 % of its
+        # samples) and bins far below fp32 resolution, which log(S + 1e-7) amplifies: torch's own
+        # fp32 path misses float64 by 1.2e-3 on it (reported as a diagnostic), so that class gets
+        # MSS_SILENT_TOL. The same pair with the silence filled by low-level noise is the
+        # non-silent class and must meet north_star's 1e-4.
         gap = _torch_fp32_mss_gap(p0.detach()[0].cpu().numpy(), tgt[0].cpu().numpy(), sizes, ref)
-        tol = max(1e-4, 1.5 * gap)
+        t1 = tgt[:1] + 1e-3 * torch.from_numpy(rng.standard_normal((1, L)).astype(np.float32)).to(dev)
+        l1 = spectral.multiscale_spectral_loss(p0.detach(), t1, sizes=sizes)
+        ref1, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
+                                                   t1[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
+        rel1 = abs(l1.item() - ref1) / abs(ref1)
+        ok = rel <= MSS_SILENT_TOL and rel1 <= 1e-4
         extra["parity"] = {"pair": 0, "loss": l0.item(), "oracle": ref, "rel_err": rel,
-                           "torch_fp32_rel_err": gap, "tol": tol,
-                           **_verdict(rel <= tol, f"multi-scale loss of pair 0: {l0.item()} vs "
-                                                  f"oracle {ref} (rel {rel:.2e} > {tol:.2e})", args)}
+                           "tol": MSS_SILENT_TOL, "torch_fp32_rel_err": gap,
+                           "nonsilent": {"loss": l1.item(), "oracle": ref1, "rel_err": rel1, "tol": 1e-4},
+                           **_verdict(ok, f"multi-scale loss of pair 0: rel {rel:.2e} (bar {MSS_SILENT_TOL:.0e}),"
+                                          f" non-silent rel {rel1:.2e} (bar 1e-4)", args)}
     return [_line("multi-scale spectral loss fwd+grad clip-pairs/s, 10 s @ 22.05 kHz, 6 FFT sizes",
                   world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
                    "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
                   _roof(B * bpp / (kms * 1e-3) / 1e9,
-                        "mss_wave_kernel<6..10>, mss_fft2048_kernel + fold + loss reduce (pred and target each a real FFT)",
+                        "mss_multi_kernel (n = 64..1024 in one launch), mss_fft2048_kernel, ordered slab sum + fold + loss reduce (pred and target each a real FFT)",
                         B * bpp, traffic=_mss_traffic()), cpu, extra)]
 
 

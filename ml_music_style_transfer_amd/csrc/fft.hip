@@ -1012,6 +1012,7 @@ __global__ __launch_bounds__(64 * FMW, 4) void stft_fm_kernel(const float* __res
     STAMP(6);
   }
 }
+
 // ---------------------------------------------------------------------------
 // iSTFT (librosa.istft, center=True, Hann): workgroup = 512 threads, output segment of
 // SEG = 16 samples per thread. Frames overlapping the segment are inverse-FFT'd 8 at a

@@ -78,7 +78,8 @@ __device__ __forceinline__ Bf3 split1(float x) {
   return Bf3{b0, b1, (__bf16)(r1 - (float)b1)};
 }
 
-// 4 consecutive k (k0 = 4 c8) of one row: three 8-byte stores
+// 4 consecutive k (k0 = 4 c8) of one row: three 8-byte stores (PS: elements per plane)
+template <int PS = PLANE>
 __device__ __forceinline__ void split_store4(__bf16* plane0, int row, int c8, const f32x4 v) {
   bf16x4 hi, mid, lo;
 #pragma unroll
@@ -90,11 +91,12 @@ __device__ __forceinline__ void split_store4(__bf16* plane0, int row, int c8, co
   }
   const int off = pl_off(row, c8 >> 1) + 4 * (c8 & 1);
   *reinterpret_cast<bf16x4*>(plane0 + off) = hi;
-  *reinterpret_cast<bf16x4*>(plane0 + PLANE + off) = mid;
-  *reinterpret_cast<bf16x4*>(plane0 + 2 * PLANE + off) = lo;
+  *reinterpret_cast<bf16x4*>(plane0 + PS + off) = mid;
+  *reinterpret_cast<bf16x4*>(plane0 + 2 * PS + off) = lo;
 }
 
 // 8 consecutive k (quad q) of one row from two units: three 16-byte stores
+template <int PS = PLANE>
 __device__ __forceinline__ void split_store8(__bf16* plane0, int row, int q, const f32x4 v0,
                                              const f32x4 v1) {
   bf16x8 hi, mid, lo;
@@ -107,16 +109,17 @@ __device__ __forceinline__ void split_store8(__bf16* plane0, int row, int q, con
   }
   const int off = pl_off(row, q);
   *reinterpret_cast<bf16x8*>(plane0 + off) = hi;
-  *reinterpret_cast<bf16x8*>(plane0 + PLANE + off) = mid;
-  *reinterpret_cast<bf16x8*>(plane0 + 2 * PLANE + off) = lo;
+  *reinterpret_cast<bf16x8*>(plane0 + PS + off) = mid;
+  *reinterpret_cast<bf16x8*>(plane0 + 2 * PS + off) = lo;
 }
 
+template <int PS = PLANE>
 __device__ __forceinline__ Split3 ld_planes(const __bf16* base, int row, int q) {
   const __bf16* p = base + pl_off(row, q);
   Split3 s;
   s.h = *reinterpret_cast<const bf16x8*>(p);
-  s.m = *reinterpret_cast<const bf16x8*>(p + PLANE);
-  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PLANE);
+  s.m = *reinterpret_cast<const bf16x8*>(p + PS);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PS);
   return s;
 }
 
@@ -189,6 +192,7 @@ struct GP {
   int accumulate;
   // split-K slab
   float* ws;
+  int wide;  // conv / dgrad on the 128 x 256 kernel (gemm_w_kernel)
   // stream-K (sk_L > 0): the grid's G workgroups each run sk_L consecutive iterations of the
   // flattened (tile, 32-deep K tile) space of sk_I = tiles * nk iterations
   long long sk_L, sk_I;
@@ -478,9 +482,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   auto mfma_tile = [&]() __attribute__((always_inline)) {
-    // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
     const __bf16* Ap = reinterpret_cast<const __bf16*>(lds);
     const __bf16* Bp = Ap + 3 * PLANE;
+    // 32x32x16 bf16 operand layout: lane (r32, h) supplies row r32, k = 16 s + 8 h + [0, 8)
     const int ra0 = wm * 64 + r32, rb0 = wn * 64 + r32;
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
@@ -529,7 +533,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
       // GEMM (A/B: conv fwd +5-10 %, dgrad +9-13 %, wgrad +15-25 %); left to the scheduler
       // they sink next to their wait.
       constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
-      constexpr int NMF = 48;                                    // MFMAs per tile per wave
+      constexpr int NMF = 48;                                   // MFMAs per tile per wave
       constexpr int PER = NMF / NV > 2 ? 2 : (NMF / NV < 1 ? 1 : NMF / NV);
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -602,6 +606,229 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
     }
   }
   __syncthreads();  // Cs aliases the planes the next pass (stream-K) starts writing
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wide conv/dgrad tile (round 4, MST_GEMM_WIDE=1 A/B): 128 x 256 output tile, 512 threads =
+// 8 waves (2 x 4 over 64 x 64 wave tiles), ONE workgroup per CU. The A tile (128 x 32) is loaded
+// and split once for 256 columns; the bf16 planes are double-buffered (2 x 72 KB), so iteration
+// k runs tile k's MFMAs from one buffer while it splits and stores tile k+1 (loaded one iteration
+// earlier) into the other: one workgroup barrier per K tile, and the split/store work sits beside
+// the workgroup's own MFMAs instead of relying on a second workgroup on the CU. Threads form two
+// 256-thread groups g: group g loads A units 2g, 2g+1 and the B half n0 + 128 g (all 4 units), so
+// the per-thread loader is the 128 x 128 kernel's with 6 units instead of 8.
+constexpr int BNW = 256, NTHRW = 512;
+constexpr int PLANE_BW = BNW * LDKB;              // bf16 elements per B plane (256 rows)
+constexpr int STAGE_BF = 3 * PLANE + 3 * PLANE_BW;  // bf16 elements per stage (72 KB)
+constexpr int LDS_W_FLOATS = STAGE_BF;            // two stages = 144 KB; the 128 KB epilogue tile aliases
+static_assert(BM * BNW <= LDS_W_FLOATS, "epilogue tile must fit the two stages");
+
+template <int TAPS, int AMODE, bool DUAL>
+__device__ __forceinline__ void tile_pass_w(const GP& p, float* lds, int m_t, int n_t, int kt0,
+                                            int kt1, int split, int tid) {
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);  // thread group (B half)
+  const int t = tid & 255;
+  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int m0 = m_t * BM;
+  const int nb0 = n_t * BNW + 128 * g;  // this group's B rows
+  auto km_r = [&](int u) __attribute__((always_inline)) { return (t >> 3) + 32 * u; };
+  const int km_q = t & 7;
+  const int rm_row = t & 127;
+  const int kw = __builtin_amdgcn_readfirstlane((tid >> 7) & 1);
+
+  f32x4 ra[2][2], rb[2][4];  // two register stages: 2 A units (u = 2 g + j) and 4 B units
+  const rsrc_t rA = mk_rsrc(p.A, p.nA);
+  uint32_t rowA[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int u = 2 * g + j;
+    const int m = m0 + (AMODE == 2 ? rm_row : km_r(u));
+    rowA[j] = m < p.M ? (uint32_t)(m * p.sAm + (AMODE == 2 ? 0 : 4 * km_q * p.sAc)) * 4u : OOB;
+  }
+  int tinb;
+  uint32_t colb0, colb1;
+  {
+    const int n = nb0 + rm_row;
+    const int bb = n / p.Tn;
+    const int tt = n - bb * p.Tn;
+    tinb = n < p.N ? p.ta * tt + p.tb : -(1 << 29);
+    colb0 = (uint32_t)(bb * p.sb0) * 4u;
+    colb1 = DUAL ? (uint32_t)(bb * p.sb1) * 4u : 0u;
+  }
+  auto load_tile = [&](auto S, int tap, int blk) __attribute__((always_inline)) {
+    constexpr int st_ = decltype(S)::value;
+    const bool s1 = DUAL && blk >= p.nb0;
+    const int cb = (s1 ? blk - p.nb0 : blk) * BK;
+    const int ci = cb + sel(s1, p.C0, 0);
+    const int Cs = sel(s1, p.C1, p.C0);
+    const int sA = (ci * p.sAc + tap * p.sAt) * 4;
+    if constexpr (AMODE == 1) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) ra[st_][j] = ldbs4(rA, rowA[j], sA);
+    } else if constexpr (AMODE == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ra[st_][j][i] = ldbs(rA, rowA[j], sA + i * p.sAc * 4);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          ra[st_][j][i] = ldbs(rA, rowA[0], sA + (4 * rm_quad(kw, 2 * g + j) + i) * p.sAc * 4);
+    }
+    const int tin = tinb + p.tg * tap;
+    const int ts = tin + sel(s1, p.off1, p.off0);
+    const bool ok = ((unsigned)tin < (unsigned)p.Tv) & ((unsigned)ts < (unsigned)sel(s1, p.T1, p.T0));
+    const uint32_t lo = ok ? sel(s1, colb1, colb0) + (uint32_t)ts * 4u : OOB;
+    const float* xs = sel(DUAL && s1, p.x1, p.x0);
+    const long long ns = sel(DUAL && s1, p.nx1, p.nx0);
+    const int scb = sel(s1, p.sc1, p.sc0) * 4;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = cb + 4 * rm_quad(kw, u) + i;
+        rb[st_][u][i] = ldbs(mk_rsrc(xs, c < Cs ? ns : 0), lo, c * scb);
+      }
+  };
+  auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
+    constexpr int st = decltype(S)::value;
+    __bf16* Ap = reinterpret_cast<__bf16*>(lds) + buf * STAGE_BF;
+    __bf16* Bp = Ap + 3 * PLANE;
+    if constexpr (AMODE == 2) {  // this group's A quads 4 kw + 2 g + (0, 1): one pair
+      split_store8<PLANE>(Ap, rm_row, 2 * kw + g, ra[st][0], ra[st][1]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) split_store4<PLANE>(Ap, km_r(2 * g + j), km_q, ra[st][j]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u += 2)
+      split_store8<PLANE_BW>(Bp, 128 * g + rm_row, 2 * kw + u / 2, rb[st][u], rb[st][u + 1]);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int r32 = lane & 31;
+  const int h = lane >> 5;
+  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + buf * STAGE_BF;
+    const __bf16* Bp = Ap + 3 * PLANE;
+    const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, 2 * s + h), b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 * s + h);
+      {
+        const Split3 a0 = ld_planes<PLANE>(Ap, ra0, 2 * s + h);
+        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+      }
+      {
+        const Split3 a1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 * s + h);
+        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+      }
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  if (kt0 < kt1) {
+    int tap = kt0 / p.nbT, blk = kt0 - tap * p.nbT;
+    auto advance = [&]() __attribute__((always_inline)) {
+      if (++blk == p.nbT) {
+        blk = 0;
+        ++tap;
+      }
+    };
+    // tile i (from kt0) lives in register stage i & 1 and LDS buffer i & 1
+    load_tile(I0{}, tap, blk);
+    advance();
+    load_tile(I1{}, tap, blk);
+    advance();
+    store_tile(I0{}, 0);
+    __syncthreads();
+    // Tile i's MFMAs from one buffer, the split and store of tile i + 1 into the other, with the
+    // split's VALU and LDS writes and the next loads interleaved between the MFMAs
+    // (sched_group_barrier). Running the two groups' phases in opposite order instead (one wave
+    // per SIMD on MFMAs while the other splits) measured 9 % slower in the step (round 4).
+    auto step = [&](auto S) __attribute__((always_inline)) {
+      constexpr int sb = decltype(S)::value;  // this tile's stage / buffer
+      load_tile(S, tap, blk);                 // tile i + 2 into the stage tile i left
+      advance();
+      mfma_tile(sb);
+      store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);  // tile i + 1
+      constexpr int NV = (AMODE == 1 ? 2 : 8) + 16;                // VMEM loads per tile
+#pragma unroll
+      for (int i = 0; i < 48; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
+        if (i < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU (split)
+        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+      }
+      __syncthreads();
+    };
+    for (int kt = kt0; kt < kt1; kt += 2) {
+      step(I0{});
+      if (kt + 1 < kt1) step(I1{});
+    }
+  }
+
+  // ---- epilogue: accumulators -> LDS tile (128 x 256) -> row-contiguous stores ----
+  float* Cs = lds;
+  const int nl = tid & (BNW - 1);
+  const int n = n_t * BNW + nl;
+  __shared__ float s_bias_w[BM];
+  const bool use_bias = p.splitk <= 1 && p.bias != nullptr;
+  if (use_bias && tid < BM) s_bias_w[tid] = m0 + tid < p.M ? p.bias[m0 + tid] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl2 = 128 * g + wn * 64 + j * 32 + r32;
+        Cs[ml * BNW + nl2] = acc[i][j][r];
+      }
+  __syncthreads();
+  if (n < p.N) {
+    for (int ml = tid >> 8; ml < BM; ml += NTHRW / BNW) {
+      const int m = m0 + ml;
+      if (m >= p.M) break;
+      const float v = Cs[ml * BNW + nl];
+      if (p.splitk > 1) p.ws[((long long)split * p.M + m) * p.N + n] = v;
+      else conv_store_b(p, m, n, v, use_bias ? s_bias_w[ml] : 0.f);
+    }
+  }
+}
+
+template <int TAPS, int AMODE, bool DUAL>
+__global__ __launch_bounds__(NTHRW, 1) void gemm_w_kernel(const GP p) {
+  __shared__ __attribute__((aligned(16))) float lds[LDS_W_FLOATS];
+  const int nx = (p.N + BNW - 1) / BNW, ny = (p.M + BM - 1) / BM;
+  const int W = nx * ny * (int)gridDim.z;
+  const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
+  const int split = t / (nx * ny);
+  int m_t, n_t;
+  tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
+  const int kt0 = (int)((long long)split * p.nk / p.splitk);
+  const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
+  tile_pass_w<TAPS, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
+}
+
+static int gemm_wide() {  // MST_GEMM_WIDE=1: conv / dgrad on the 128 x 256 kernel (A/B)
+  static const int v = [] {
+    const char* e = getenv("MST_GEMM_WIDE");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
 }
 
 // Schedules. Data-parallel / split-K: one (tile, split) per workgroup, grid (nx, ny, splitk).
@@ -740,9 +967,9 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
 // a workgroup's time is ~ (its K tiles) x tau. A trailing partial wave of <= 256 workgroups
 // runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave. Split-K
 // adds a slab round trip (s + 2 passes over M x N floats at ~5 TB/s) plus a launch.
-int choose_splitk(int M, int N, int nk, int req, int occ) {
+int choose_splitk(int M, int N, int nk, int req, int occ, int bn = BN) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
-  const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, BN);
+  const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, bn);
   static const double tau_env = [] {  // dev override for tuning (MST_SPLITK_TAU seconds)
     const char* e = getenv("MST_SPLITK_TAU");
     return e ? atof(e) : 0.0;
@@ -795,11 +1022,12 @@ void choose_sched(GP& p, int req) {
     if (sk) G = SK_G;
   }
   if (G > 0) {
+    p.wide = 0;
     p.splitk = 1;
     p.sk_I = tiles * p.nk;
     p.sk_L = (p.sk_I + G - 1) / G;
   } else {
-    p.splitk = choose_splitk(p.M, p.N, p.nk, req, 2);
+    p.splitk = p.wide ? choose_splitk(p.M, p.N, p.nk, req, 1, BNW) : choose_splitk(p.M, p.N, p.nk, req, 2);
   }
 }
 
@@ -826,8 +1054,13 @@ int launch(const GP& p, hipStream_t st, int taps) {
   dim3 grid(ceil_div(p.N, BN), ceil_div(p.M, BM), p.splitk);
   if (p.sk_L > 0) grid = dim3((unsigned)((p.sk_I + p.sk_L - 1) / p.sk_L), 1, 1);
   dim3 block(NTHR);
+  const bool wide = !WG && p.wide && p.sk_L == 0;
+  const dim3 wgrid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk), wblock(NTHRW);
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
-  if (!WG && p.dual)                                                                 \
+  if (wide) {                                                                        \
+    if (p.dual) hipLaunchKernelGGL((gemm_w_kernel<TP, AM, true>), wgrid, wblock, 0, st, p); \
+    else hipLaunchKernelGGL((gemm_w_kernel<TP, AM, false>), wgrid, wblock, 0, st, p); \
+  } else if (!WG && p.dual)                                                          \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, !WG>), grid, block, 0, st, p);       \
   else                                                                               \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, false>), grid, block, 0, st, p);
@@ -958,6 +1191,7 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.drop_p = d->drop_p;
   p.seed = d->seed;
   p.seed_dev = reinterpret_cast<const unsigned long long*>(d->seed_dev);
+  p.wide = gemm_wide();
   choose_sched(p, d->splitk);
   return MST_OK;
 }

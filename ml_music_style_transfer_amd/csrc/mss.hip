@@ -7,15 +7,16 @@
 //
 // (oracle/spectral_ref.py:multiscale_spectral_loss_grad is the float64 statement.)
 //
-// One launch per size. A workgroup owns R = 4096 consecutive samples of one clip's padded
+// Sizes n = 64 .. 1024 run in ONE launch (mss_multi_kernel, grid z = size) and n = 2048 in
+// mss_fft2048_kernel (fft.hip). A workgroup owns R = 4096 consecutive samples of one clip's padded
 // signal and computes every frame that overlaps them (3 halo frames recomputed at the left
 // edge), so the gradient is accumulated on chip and written once: no atomics, no spectra in
 // HBM. Every frame of pred and of target is transformed on its own as a real FFT (an n/2-point
 // complex transform of the even/odd samples plus the post-twist), in place inside one wave;
 // the two gradient frames of a frame pair are packed into one Hermitian-completed inverse
 // transform (real part = frame a, imaginary part = frame b).
-// Deterministic: fixed summation order everywhere; per-size launches accumulate into dpred
-// in stream order, reflect-pad edges are folded in by a final kernel.
+// Deterministic: fixed summation order everywhere; each size writes its own gradient slab and
+// mss_sum_kernel adds the slabs in size order; reflect-pad edges are folded in by a final kernel.
 #include <cstdlib>
 
 #include "common.h"
@@ -150,23 +151,40 @@ __device__ __forceinline__ void wave_fft(c2* s, const c2* qt, int lane) {
   }
 }
 
+#ifndef MST_MSS_BW
+#define MST_MSS_BW 1024  // complex per wave buffer for n <= MST_MSS_BW (A/B: 512 halves LDS and registers)
+#endif
+#ifndef MST_MSS_OCC
+#define MST_MSS_OCC 4
+#endif
+constexpr int MSS_W = 4;  // waves per workgroup
 template <int LOG2N>
-__global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(const MssArgs a) {
+struct MssGeom {
+  static constexpr int N = 1 << LOG2N;
+  static constexpr int BW = N > MST_MSS_BW ? N : MST_MSS_BW;  // complex per wave buffer
+  // LDS bytes: wave buffers, the two quarter tables, the window, the reduction
+  static constexpr int LDS = MSS_W * BW * 8 + (N / 4) * 8 + (N / 8) * 8 + N * 4 + 2 * MSS_W * 4;
+};
+constexpr int MSS_LDS_MAX = MssGeom<10>::LDS;  // the largest size the fused launch serves
+
+// One workgroup (w, b) of size n = 2^LOG2N; lds: MssGeom<LOG2N>::LDS bytes, 16-byte aligned.
+template <int LOG2N>
+__device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, char* lds) {
   constexpr int N = 1 << LOG2N, H = N / 4, HALF = N / 2, NBIN = HALF + 1;
-  constexpr int W = 4;                       // waves per workgroup
-  constexpr int BW = N > 1024 ? N : 1024;    // complex per wave buffer
+  constexpr int W = MSS_W;                   // waves per workgroup
+  constexpr int BW = MssGeom<LOG2N>::BW;     // complex per wave buffer
   constexpr int FB = BW / N;                 // transforms per pass
   constexpr int GF = 2 * FB;                 // frames per wave per round
   constexpr int RF = W * GF;                 // frames per round
   constexpr int NE = (FB * NBIN + 63) / 64;  // spectrum entries per lane
   constexpr int OWN = RWIN / 256;            // owned samples per thread
-  __shared__ __attribute__((aligned(16))) c2 buf[W * BW];
-  __shared__ c2 qt[N / 4];
-  __shared__ c2 qth[N / 8];  // quarter table of the n/2-point forward transforms
-  __shared__ __attribute__((aligned(16))) float hw[N];
-  __shared__ float red[2][W];
+  c2* buf = reinterpret_cast<c2*>(lds);                                   // [W * BW]
+  c2* qt = buf + W * BW;                                                  // [N / 4]
+  c2* qth = qt + N / 4;  // quarter table of the n/2-point forward transforms  [N / 8]
+  float* hw = reinterpret_cast<float*>(qth + N / 8);                     // [N]
+  float (*red)[W] = reinterpret_cast<float (*)[W]>(hw + N);              // [2][W]
 
-  const int w = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = (int)a.L;
   const float* p = a.pred + (long long)b * a.L;
@@ -335,25 +353,64 @@ __global__ __launch_bounds__(256, LOG2N == 11 ? 2 : 4) void mss_wave_kernel(cons
     a.partial[((long long)b * a.nwg + w) * 2 + 1] = sl;
   }
   if (!grad) return;
+  // this size's gradient slab (the sizes are summed in order by mss_sum_kernel)
   float* dp = a.dpred + (long long)b * a.L;
   float* ed = a.edges + (long long)b * N;
   const int own_hi = min(own_lo + RWIN, L + N);
-  // the previous sizes' sums, loaded together up front (clamped in range; a load inside the
-  // per-sample branch below made hipcc wait for each one: 16 serialised round trips)
-  float prev[OWN];
-#pragma unroll
-  for (int i = 0; i < OWN; ++i)
-    prev[i] = dp[min(max(own_lo + tid + 256 * i - HALF, 0), L - 1)];  // unconditional: no join
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     // one store per sample to the address picked by selects (stores under the three-way
     // branch each waited for every earlier store: vmcnt counts stores on gfx950)
     const int pp = own_lo + tid + 256 * i;
     const int x = pp - HALF;
-    const float v0 = acc[i];
     float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
-    const float val = (x >= 0 && x < L && a.accumulate) ? prev[i] + v0 : v0;
-    if (pp < own_hi) *dst = val;
+    if (pp < own_hi) *dst = acc[i];
+  }
+}
+
+// Sizes n = 64 .. 1024 of one loss call in ONE launch: blockIdx.z picks the size (its workgroups
+// are (w < nwg, b)), so the per-size grids (1.7 residency waves each at config 5) no longer end in
+// a partial wave apiece and no launch gap separates the sizes. Every size writes its own gradient
+// slab; mss_sum_kernel adds them in size order (the order the per-size launches accumulated in).
+struct MssMulti {
+  MssArgs s[8];
+  int lg[8];
+  int nsz;
+};
+
+__global__ __launch_bounds__(256, 4) void mss_multi_kernel(const MssMulti m) {
+  __shared__ __attribute__((aligned(16))) char lds[MSS_LDS_MAX];
+  const int z = blockIdx.z;
+  const MssArgs& a = m.s[z];
+  const int w = blockIdx.x, b = blockIdx.y;
+  if (w >= a.nwg) return;  // whole workgroup, before any barrier
+  switch (m.lg[z]) {
+    case 6: mss_wave_body<6>(a, w, b, lds); break;
+    case 7: mss_wave_body<7>(a, w, b, lds); break;
+    case 8: mss_wave_body<8>(a, w, b, lds); break;
+    case 9: mss_wave_body<9>(a, w, b, lds); break;
+    default: mss_wave_body<10>(a, w, b, lds); break;
+  }
+}
+
+// dpred[i] = ((slab_0 + slab_1) + ...) [i], the sizes in call order (the per-size launches' order);
+// slabs are `stride` floats apart (a multiple of 4, 16-byte aligned); vec: dpred 16-byte aligned
+__global__ __launch_bounds__(256) void mss_sum_kernel(const float* __restrict__ slabs, long long n,
+                                                      long long stride, int nsz, int vec,
+                                                      float* __restrict__ dpred) {
+  const long long n4 = vec ? n >> 2 : 0;
+  const f32x4* sl = reinterpret_cast<const f32x4*>(slabs);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    f32x4 v = sl[i];
+    for (int s = 1; s < nsz; ++s) v += sl[s * (stride >> 2) + i];
+    reinterpret_cast<f32x4*>(dpred)[i] = v;
+  }
+  for (long long i = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = slabs[i];
+    for (int s = 1; s < nsz; ++s) v += slabs[s * stride + i];
+    dpred[i] = v;
   }
 }
 
@@ -455,16 +512,6 @@ __global__ __launch_bounds__(256) void mss_finish_kernel(const FinishArgs a) {
   else mss_loss(a.l);
 }
 
-// MST_MSS_REG=0: n = 2048 on mss_wave_kernel instead of the register-resident fft1024_v2
-// kernel (fft.hip; A/B)
-bool mss_reg() {
-  static const bool v = [] {
-    const char* e = getenv("MST_MSS_REG");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 int log2i(int n) {
   int l = 0;
   while ((1 << l) < n) ++l;
@@ -474,7 +521,7 @@ int log2i(int n) {
 struct Plan {
   int nsz;
   int n[8], T[8], nwg[8];
-  long long part_off[8], edge_off[8];
+  long long part_off[8], edge_off[8], slab_off[8], slab_stride;
   size_t bytes;
 };
 
@@ -494,7 +541,11 @@ int make_plan(int64_t B, int64_t L, int32_t n_sizes, const int32_t* sizes, Plan&
     pl.edge_off[s] = edge;
     edge += B * n;
   }
-  pl.bytes = (size_t)(part + edge) * sizeof(float);
+  // per-size gradient slabs (B, L), summed in size order by mss_sum_kernel
+  pl.slab_stride = (B * L + 3) / 4 * 4;
+  const long long slab0 = (part + edge + 3) / 4 * 4;
+  for (int s = 0; s < n_sizes; ++s) pl.slab_off[s] = slab0 + s * pl.slab_stride;
+  pl.bytes = (size_t)(slab0 + n_sizes * pl.slab_stride) * sizeof(float);
   for (int s = 0; s < n_sizes; ++s) pl.edge_off[s] += part;
   return 0;
 }
@@ -518,6 +569,10 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
   MST_REQUIRE(pred && target && loss && ws && ws_bytes >= pl.bytes && B <= 65535);
   hipStream_t st = (hipStream_t)stream;
   float* w = (float*)ws;
+  MST_REQUIRE(((uintptr_t)ws & 15) == 0);
+  MssMulti mm;
+  mm.nsz = 0;
+  unsigned max_nwg = 0;
   for (int s = 0; s < pl.nsz; ++s) {
     MssArgs a;
     a.pred = pred;
@@ -528,22 +583,31 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     a.alpha = alpha;
     a.eps = eps;
     a.inv_cnt = (float)(1.0 / ((double)B * pl.T[s] * (pl.n[s] / 2 + 1)));
-    a.dpred = dpred;
-    a.accumulate = s > 0;
+    a.dpred = dpred ? w + pl.slab_off[s] : nullptr;  // this size's slab
+    a.accumulate = 0;
     a.edges = w + pl.edge_off[s];
     a.partial = w + pl.part_off[s];
-    dim3 grid(pl.nwg[s], (unsigned)B);
-    switch (log2i(pl.n[s])) {
-      case 6: mss_wave_kernel<6><<<grid, 256, 0, st>>>(a); break;
-      case 7: mss_wave_kernel<7><<<grid, 256, 0, st>>>(a); break;
-      case 8: mss_wave_kernel<8><<<grid, 256, 0, st>>>(a); break;
-      case 9: mss_wave_kernel<9><<<grid, 256, 0, st>>>(a); break;
-      case 10: mss_wave_kernel<10><<<grid, 256, 0, st>>>(a); break;
-      default:
-        if (mss_reg()) mss_fft2048_launch(a, grid.x, grid.y, st);
-        else mss_wave_kernel<11><<<grid, 256, 0, st>>>(a);
-        break;
+    const int lg = log2i(pl.n[s]);
+    if (lg == 11) {  // register-resident fft1024_v2 kernel (fft.hip)
+      mss_fft2048_launch(a, (unsigned)pl.nwg[s], (unsigned)B, st);
+      MST_CHECK_LAUNCH();
+    } else {
+      mm.s[mm.nsz] = a;
+      mm.lg[mm.nsz] = lg;
+      ++mm.nsz;
+      max_nwg = max_nwg > (unsigned)pl.nwg[s] ? max_nwg : (unsigned)pl.nwg[s];
     }
+  }
+  if (mm.nsz > 0) {
+    hipLaunchKernelGGL(mss_multi_kernel, dim3(max_nwg, (unsigned)B, (unsigned)mm.nsz), dim3(256), 0, st, mm);
+    MST_CHECK_LAUNCH();
+  }
+  if (dpred) {
+    const long long n = B * L;
+    const long long blocks = (n / 4 + 256) / 256;
+    hipLaunchKernelGGL(mss_sum_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st,
+                       (const float*)(w + pl.slab_off[0]), n, pl.slab_stride, pl.nsz,
+                       ((uintptr_t)dpred & 15) == 0 ? 1 : 0, dpred);
     MST_CHECK_LAUNCH();
   }
   FinishArgs fa;

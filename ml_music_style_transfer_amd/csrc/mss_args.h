@@ -1,4 +1,4 @@
-// Arguments of the multi-scale spectral loss kernels (mss.hip), shared with the n = 1024 kernel in
+// Arguments of the multi-scale spectral loss kernels (mss.hip), shared with the n = 2048 kernel in
 // fft.hip, which reuses fft.hip's register-resident 1024-point FFT.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -12,11 +12,10 @@ struct MssArgs {
   int T, nwg;
   float alpha, eps, inv_cnt;
   float* dpred;        // (B, L) or null
-  int accumulate;      // add into dpred (sizes after the first)
+  int accumulate;      // add into dpred instead of writing it (0 on the slab path)
   float* edges;        // (B, n): gradient of the reflect-pad samples, head n/2 then tail n/2
   float* partial;      // (B, nwg, 2): per-workgroup sums of |dS| and |dlogS|
 };
 
-// n = 1024: grid (nwg, B), 256 threads (fft.hip)
-// n = 2048: the same with one radix-2 step around two fft1024 (fft.hip)
+// n = 2048: grid (nwg, B), 256 threads, one radix-2 step around two fft1024 (fft.hip)
 void mss_fft2048_launch(const MssArgs& a, unsigned nwg, unsigned B, hipStream_t st);

@@ -272,27 +272,33 @@ __global__ __launch_bounds__(256) void bias_rows_kernel(const float* __restrict_
   db[c] = accumulate ? db[c] + s : s;
 }
 
-// db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one wave per channel, four per block. A wave
-// covers 64 / G rows of G-lane segments per step (G = 16, 32 or 64 with G >= T or G = 64), so
-// the short rows of the dense layers (T = 15 at B = 32) keep most lanes busy; lane partials and
-// the wave reduction run in a fixed order (deterministic). The previous form (one 256-thread
-// block per channel, threads along t) left 241 of 256 threads idle at T = 15.
+// db[c] = scale * sum_{b,t} dy[b][c][t] (+ db[c]); one 256-thread workgroup per channel over the
+// flattened (b, t) index j = b T + t: thread k sums j = k, k + 256, ... (coalesced within each
+// row, every thread busy whatever T is), then a fixed-order wave and workgroup reduction
+// (deterministic). Round 3's one-wave-per-channel form had a single wave walk all B rows of a
+// channel (34 us per call at 14 calls per step, latency-bound).
 __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ dy, int B, int C,
                                                         int T, float scale, float* __restrict__ db,
                                                         int accumulate) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;  // whole wave
-  const int G = T <= 16 ? 16 : (T <= 32 ? 32 : 64);
-  const int R = 64 / G, sub = lane / G, tl = lane - sub * G;
-  float s = 0.f;
-  for (int b = sub; b < B; b += R) {
-    const float* r = dy + ((long long)b * C + c) * T;
-    for (int t = tl; t < T; t += G) s += r[t];
+  __shared__ float part[4];
+  const int c = blockIdx.x;
+  const int n = B * T;
+  float s0 = 0.f, s1 = 0.f;
+  int j = threadIdx.x;
+  for (; j + 256 < n; j += 512) {  // two independent chains
+    const int b0 = j / T, b1 = (j + 256) / T;
+    s0 += dy[((long long)b0 * C + c) * T + (j - b0 * T)];
+    s1 += dy[((long long)b1 * C + c) * T + (j + 256 - b1 * T)];
   }
-  s = wave_sum(s);
-  if (lane == 0) {
-    float v = s * scale;
+  if (j < n) {
+    const int b0 = j / T;
+    s0 += dy[((long long)b0 * C + c) * T + (j - b0 * T)];
+  }
+  const float s = wave_sum(s0 + s1);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = ((part[0] + part[1]) + (part[2] + part[3])) * scale;
     if (accumulate) v += db[c];
     db[c] = v;
   }
@@ -570,9 +576,9 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
 
 int mst_bias_grad_f32(const float* dy, int32_t B, int32_t C, int32_t T, float scale, float* db,
                       int32_t accumulate, void* stream) {
-  MST_REQUIRE(dy && db && B > 0 && C > 0 && T > 0);
-  hipLaunchKernelGGL(bias_grad_kernel, dim3((C + 3) / 4), dim3(256), 0, (hipStream_t)stream, dy, B,
-                     C, T, scale, db, accumulate);
+  MST_REQUIRE(dy && db && B > 0 && C > 0 && T > 0 && (long long)B * T < (1ll << 30));
+  hipLaunchKernelGGL(bias_grad_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, dy, B, C, T, scale,
+                     db, accumulate);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
