@@ -57,15 +57,23 @@ struct Split3 {
 // epilogue tile aliases it), so two workgroups fit per CU: the tile loop stores, syncs, runs the
 // MFMAs, syncs, and the other workgroup on the CU fills the store phase.
 // Plane rows are 64 B (32 bf16, no padding) with the four 16-byte quads of row r XOR-swizzled by
-// (r >> 2) & 3: a 16-row fragment read (16-byte lanes) and a 4-row k-major write (8-byte lanes,
-// 8 per row) each cover every bank once, and the row-major writes pair two k quads into one
-// 16-byte store per plane (their unit order, rm_quad, makes a thread's quads adjacent).
+// swz(r) = r2 | (r1 ^ r3) << 1 (r_i: bit i of r). The banking rules (MI355X_MICROARCH.md, LDS
+// table) it satisfies: a ds_read_b128 fragment read (16-row lane groups {0-3, 12-15, 20-27} and
+// {4-11, 16-19, 28-31}, 64 banks) and a k-major ds_write_b64 (16 contiguous lanes = 2 rows, 32
+// banks) each touch every bank once, and so does a row-major ds_write_b128 (8 contiguous lanes =
+// 8 rows, 32 banks: rows of one parity need distinct swizzles). The round-3 swizzle (r >> 2) & 3
+// made that last one 2-way (PMC: 20 % of conv and 33 % of dgrad LDS cycles were conflicts,
+// profiles/r04/pmc_gemm_m4_summary.txt). The row-major writes pair two k quads into one 16-byte
+// store per plane (their unit order, rm_quad, makes a thread's quads adjacent).
 constexpr int LDKB = BK;
 constexpr int PLANE = BM * LDKB;  // bf16 elements per plane (BM == BN)
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+__device__ __forceinline__ int pl_swz(int row) {
+  return ((row >> 2) & 1) | (((row >> 1) ^ (row >> 3)) & 1) << 1;
+}
 __device__ __forceinline__ int pl_off(int row, int q) {  // element offset of (row, 16-B quad q)
-  return row * LDKB + 8 * (q ^ ((row >> 2) & 3));
+  return row * LDKB + 8 * (q ^ pl_swz(row));
 }
 
 struct Bf3 {
@@ -823,10 +831,10 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_w_kernel(const GP p) {
   tile_pass_w<TAPS, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
 }
 
-static int gemm_wide() {  // MST_GEMM_WIDE=1: conv / dgrad on the 128 x 256 kernel (A/B)
+static int gemm_wide() {  // conv / dgrad on the 128 x 256 kernel; MST_GEMM_WIDE=0: the 128 x 128 one
   static const int v = [] {
     const char* e = getenv("MST_GEMM_WIDE");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] == '0') ? 0 : 1;
   }();
   return v;
 }

@@ -11,7 +11,7 @@ def kernels(text):
         name = m.group(1)
         if name.startswith(".") or name.startswith("_Z") is False:
             continue
-        end = text.find("s_endpgm", m.end())
+        end = text.find(".Lfunc_end", m.end())  # a kernel can hold several s_endpgm
         yield name, text[m.end():end]
 
 
@@ -22,15 +22,15 @@ def loop_of(body):
         return None
     hdr = None
     for i in range(first, -1, -1):
-        if re.match(r"^\.LBB\S+:.*Loop Header", lines[i]):
-            hdr = i
+        if "Loop Header" in lines[i]:
+            hdr = i if lines[i].startswith(".LBB") else i - 1  # the comment may have its own line
             break
     if hdr is None:
         return None
     label = lines[hdr].split(":")[0]
     end = None
     for i in range(first, len(lines)):
-        if re.search(r"s_cbranch\w*\s+" + re.escape(label) + r"\s*$", lines[i]):
+        if re.search(r"s_c?branch\w*\s+" + re.escape(label) + r"(\s|$)", lines[i]):
             end = i
     return lines[hdr:end + 1] if end else None
 
