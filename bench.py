@@ -124,7 +124,7 @@ def cpu_baseline(B=32, steps=1):
 
 
 def gemm_traffic():
-    """HBM-side bytes per gemm_kernel launch from this round's PMC passes (tools/pmc_traffic.py
+    """HBM-side bytes per GEMM launch (gemm_kernel and gemm_w_kernel) from this round's PMC passes (tools/pmc_traffic.py
     over `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` runs of this bench), newest round
     first. Returns (bytes or None, source note)."""
     pdir = os.path.join(ROOT, "profiles")
@@ -138,7 +138,7 @@ def gemm_traffic():
             return round(d["traffic_bytes_per_launch"]), (
                 f"profiles/{r}/gemm_traffic.json ({d.get('build', 'build not recorded')}): "
                 "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes over this bench, "
-                "2 x fetch + write per gemm_kernel launch")
+                "2 x fetch + write per GEMM launch")
     return None, None
 
 
@@ -349,7 +349,8 @@ def main():
                    "sample_rate": SR, "n_fft": 2048, "hop": HOP, "parallelism": f"dp{world}"},
         "roofline": {
             "bound": "mfma",
-            "kernel": ("gemm_kernel (implicit GEMM, all conv/linear fwd/dgrad/wgrad; fp32 operands "
+            "kernel": ("gemm_w_kernel (128 x 256 tiles: conv/linear fwd and dgrad) and gemm_kernel "
+                       "(128 x 128: wgrad, stream-K) (implicit GEMM; fp32 operands "
                        + ("split into 3 bf16 pieces, 6 x v_mfma_f32_32x32x16_bf16 per 16-deep k step)"
                           if products > 1 else "v_mfma_f32_32x32x2_f32)")),
             "achieved": round(achieved, 2),

@@ -30,7 +30,7 @@ def per_kernel(d, counter):
 
 def main():
     fd, wd, out = sys.argv[1:4]
-    sub = sys.argv[4] if len(sys.argv) > 4 else "gemm_kernel"
+    sub = sys.argv[4] if len(sys.argv) > 4 else "gemm_"  # gemm_kernel and gemm_w_kernel
     fe, wr = per_kernel(fd, "FETCH_SIZE"), per_kernel(wd, "WRITE_SIZE")
     rows = {}
     tf = tw = n = 0
