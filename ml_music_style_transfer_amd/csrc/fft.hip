@@ -1683,7 +1683,7 @@ int gl_synth_launch(const float2* cur, const float2* prev, const float* mag, flo
 
 // ---------------------------------------------------------------------------
 // Multi-scale spectral loss, n = 2048 (mss.hip has the other sizes and the plan): the same
-// ownership, frame pairing and ordered overlap-add as mss_wave_kernel, with every transform a
+// ownership, frame pairing and ordered overlap-add as mss_wave_body (mss.hip), with every transform a
 // register-resident fft1024_v2.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int mss_reflect(int i, int L) {
