@@ -59,7 +59,9 @@ def _worker(rank, world, port, q):
     issued_in_backward = r.next
     dp.finish_gradients(net)
     torch.cuda.synchronize()
-    q.put((rank, local, grad[idx].cpu(), issued_in_backward, len(r.buckets)))
+    # numpy: pickled by value (a CPU tensor travels as a shared-memory fd that the parent can only
+    # open while this process is alive)
+    q.put((rank, local.numpy(), grad[idx].cpu().numpy(), issued_in_backward, len(r.buckets)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -77,7 +79,7 @@ def test_overlapped_allreduce_two_ranks_one_gpu(cuda):
     while len(res) < world:
         try:
             rank, local, reduced, issued, nb = q.get(timeout=5)
-            res[rank] = (local, reduced, issued, nb)
+            res[rank] = (torch.from_numpy(local), torch.from_numpy(reduced), issued, nb)
         except queue.Empty:
             dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
             if dead or time.monotonic() > deadline:
@@ -109,7 +111,8 @@ def _train_worker(rank, world, port, workdir, q):
     flat, _, n = model.flat_buffers()
     idx = torch.randint(0, n, (NSAMP,), generator=torch.Generator().manual_seed(4)).to(flat.device)
     torch.cuda.synchronize()
-    q.put((rank, hp.loss_history, hp.test_loss_history, hp.best_epoch, flat[idx].cpu()))
+    q.put((rank, hp.loss_history, hp.test_loss_history, hp.best_epoch,
+           flat[idx].cpu().numpy()))  # numpy: pickled by value, no fd sharing
     dist.barrier()
     dist.destroy_process_group()
 
@@ -153,7 +156,7 @@ def test_train_main_data_parallel_two_ranks(cuda, tmp_path, monkeypatch):
         assert p.exitcode == 0
     assert res[0][0] == res[1][0] and res[0][1] == res[1][1] and res[0][2] == res[1][2]
     assert all(np.isfinite(res[0][0])) and len(res[0][0]) == 2
-    torch.testing.assert_close(res[0][3], res[1][3], rtol=0, atol=0)
+    np.testing.assert_array_equal(res[0][3], res[1][3])
     exp = tmp_path / "experiments" / "piano_test"
     assert (exp / ("checkpoint-%d.tar" % res[0][2])).exists() and (exp / "hyperparams.json").exists()
 
