@@ -42,4 +42,23 @@ __device__ __forceinline__ uint32_t mst_hash32(uint64_t seed, uint64_t idx) {
 
 __device__ __forceinline__ float lrelu(float x, float s) { return x > 0.f ? x : x * s; }
 
+// cos / sin of 2 pi m / n in double, evaluated at compile time (quadrant-reduced Taylor series)
+static constexpr double kPiD = 3.14159265358979323846264338327950288;
+static constexpr void cx_sincos_turn(long long m, long long n, double& c, double& s) {
+  m %= n;
+  if (m < 0) m += n;
+  const long long q = (4 * m) / n;                 // quadrant
+  const double x = (double)(4 * m - q * n) / (double)n * (kPiD / 2);  // [0, pi/2)
+  double x2 = x * x, ts = x, ss = x, tc = 1.0, sc = 1.0;
+  for (int k = 1; k < 16; ++k) {
+    ts *= -x2 / ((2.0 * k) * (2.0 * k + 1.0));
+    ss += ts;
+    tc *= -x2 / ((2.0 * k - 1.0) * (2.0 * k));
+    sc += tc;
+  }
+  const double cq[4] = {sc, -ss, -sc, ss}, sq[4] = {ss, sc, -ss, -sc};
+  c = cq[q];
+  s = sq[q];
+}
+
 static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }

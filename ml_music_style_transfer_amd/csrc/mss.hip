@@ -26,6 +26,21 @@ namespace {
 
 constexpr int RWIN = MSS_RWIN;  // padded samples owned per workgroup
 
+// W2048^k = (cos, -sin)(2 pi k / 2048), k < 512, evaluated at compile time (common.h)
+struct MssW2048 {
+  float2 w[512];
+};
+constexpr MssW2048 make_mss_w2048() {
+  MssW2048 t{};
+  double c = 0, s = 0;
+  for (int k = 0; k < 512; ++k) {
+    cx_sincos_turn(k, 2048, c, s);
+    t.w[k] = float2{(float)c, (float)-s};
+  }
+  return t;
+}
+__device__ constexpr MssW2048 kMssW2048 = make_mss_w2048();
+
 struct c2 {
   float x, y;
 };
@@ -190,20 +205,23 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
   const float* p = a.pred + (long long)b * a.L;
   const float* q = a.target + (long long)b * a.L;
   const bool grad = a.dpred != nullptr;
+  // twiddles and window from the compile-time W2048 quarter table (N divides 1024): W_N^r =
+  // W2048^(r 2048 / N); the periodic Hann in its sin^2 form, sin(pi j / N) = sin(2 pi m / 2048)
+  // with m = j 1024 / N < 1024 (the edge values keep their relative precision)
+  constexpr int SN = 2048 / N;
   for (int r = tid; r < N / 4; r += 256) {
-    double sn, cs;
-    sincospi(2.0 * r / N, &sn, &cs);
-    qt[r] = mk((float)cs, (float)-sn);
+    const float2 w = kMssW2048.w[r * SN];
+    qt[r] = mk(w.x, w.y);
   }
   for (int r = tid; r < N / 8; r += 256) {
-    double sn, cs;
-    sincospi(4.0 * r / N, &sn, &cs);
-    qth[r] = mk((float)cs, (float)-sn);
+    const float2 w = kMssW2048.w[2 * r * SN];
+    qth[r] = mk(w.x, w.y);
   }
   for (int j = tid; j < N; j += 256) {
-    double sn, cs;
-    sincospi(2.0 * j / N, &sn, &cs);
-    hw[j] = (float)(0.5 - 0.5 * cs);  // periodic Hann
+    const int m = j * (SN / 2), q = m >> 9;
+    const float2 w = kMssW2048.w[m & 511];
+    const float sn = q ? w.x : -w.y;  // sin(2 pi m / 2048): quarter table entry or its cosine
+    hw[j] = sn * sn;
   }
   __syncthreads();
 

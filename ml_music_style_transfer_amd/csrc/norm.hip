@@ -26,7 +26,23 @@ __device__ __forceinline__ float seg_sum(float v) {
   return v;
 }
 
-template <int NP, int G>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t in_rsrc(const float* base, long long n) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
+                                           base ? (int)(4 * n) : 0, 0x00020000);
+}
+__device__ __forceinline__ float in_ld(__amdgpu_buffer_rsrc_t rs, long long i) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * i), 0, 0));
+}
+// elements i, i + 1 (i even, 8-byte aligned) in one load
+__device__ __forceinline__ float2 in_ld2(__amdgpu_buffer_rsrc_t rs, long long i) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)(4 * i), 0, 0);
+  return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+
+// EVEN (T even, every base 8-byte aligned): a lane's element pair is one 8-byte load and one
+// 8-byte store, in or out of the row together. All loads are issued before any is used, from
+// clamped in-row addresses (a load-or-default branch per element makes hipcc wait at each join).
+template <int NP, int G, bool EVEN>
 __global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y, long long rows,
                                                      int T, float eps, float slope,
                                                      float* __restrict__ a, float* __restrict__ pooled,
@@ -35,14 +51,26 @@ __global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y
   const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / G;
   const int lane = threadIdx.x & (G - 1);
   if (row >= rows) return;
-  const float* yr = y + row * T;
+  const auto ry = in_rsrc(y, rows * T);
   float e0[NP], e1[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int i0 = 2 * lane + 2 * G * q;
+    if constexpr (EVEN) {
+      const float2 v = in_ld2(ry, row * T + (i0 < T ? i0 : 0));
+      e0[q] = v.x;
+      e1[q] = v.y;
+    } else {
+      e0[q] = in_ld(ry, row * T + (i0 < T ? i0 : 0));
+      e1[q] = in_ld(ry, row * T + (i0 + 1 < T ? i0 + 1 : 0));
+    }
+  }
   float s = 0.f;
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
-    int i0 = 2 * lane + 2 * G * q;
-    e0[q] = i0 < T ? yr[i0] : 0.f;
-    e1[q] = i0 + 1 < T ? yr[i0 + 1] : 0.f;
+    const int i0 = 2 * lane + 2 * G * q;
+    e0[q] = i0 < T ? e0[q] : 0.f;
+    e1[q] = i0 + 1 < T ? e1[q] : 0.f;
     s += e0[q] + e1[q];
   }
   s = seg_sum<G>(s);
@@ -69,8 +97,12 @@ __global__ __launch_bounds__(256) void in_fwd_kernel(const float* __restrict__ y
     int i0 = 2 * lane + 2 * G * q;
     float a0 = lrelu((e0[q] - mu) * r, slope);
     float a1 = lrelu((e1[q] - mu) * r, slope);
-    if (i0 < T) ar[i0] = a0;
-    if (i0 + 1 < T) ar[i0 + 1] = a1;
+    if constexpr (EVEN) {
+      if (i0 < T) *reinterpret_cast<float2*>(ar + i0) = make_float2(a0, a1);
+    } else {
+      if (i0 < T) ar[i0] = a0;
+      if (i0 + 1 < T) ar[i0 + 1] = a1;
+    }
     if (pr && (i0 >> 1) < Tp) pr[i0 >> 1] = (a1 > a0) ? a1 : a0;  // first index wins ties
   }
 }
@@ -114,7 +146,7 @@ __global__ __launch_bounds__(256) void in_fwd_long_kernel(const float* __restric
 
 // Backward: da = d_a + unpool(d_pool0 + d_pool1) (to the pair's argmax), dz = lrelu'(z) da,
 // dy = rstd * (dz - mean(dz) - z * mean(dz * z)).
-template <int NP, int G>
+template <int NP, int G, bool EVEN>
 __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y,
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
@@ -137,15 +169,8 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
   // whole-tensor buffer descriptors (wave-uniform: a per-row descriptor is not, and hipcc wraps
   // each load in a waterfall loop); an absent input (null) reads 0 through the range check;
   // element indices are clamped into the row and the values past it masked below
-  auto rsrc = [&](const float* base, long long n) __attribute__((always_inline)) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0,
-                                             base ? (int)(4 * n) : 0, 0x00020000);
-  };
-  const auto ry = rsrc(y, rows * T), ra = rsrc(d_a, rows * T);
-  const auto rp0 = rsrc(dp0, rows * Tp), rp1 = rsrc(dp1, rows * Tp);
-  auto ld = [&](__amdgpu_buffer_rsrc_t rs, long long i) __attribute__((always_inline)) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4 * i), 0, 0));
-  };
+  const auto ry = in_rsrc(y, rows * T), ra = in_rsrc(d_a, rows * T);
+  const auto rp0 = in_rsrc(dp0, rows * Tp), rp1 = in_rsrc(dp1, rows * Tp);
   const bool has_p = (dp0 || dp1) && Tp > 0;  // kernel-uniform
   float y0v[NP], y1v[NP], a0v[NP], a1v[NP], gpv[NP];
 #pragma unroll
@@ -153,11 +178,19 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
     const int i0 = 2 * lane + 2 * G * q;
     const long long e0 = row * T + (i0 < T ? i0 : 0), e1 = row * T + (i0 + 1 < T ? i0 + 1 : 0);
     const long long ep = row * Tp + ((i0 >> 1) < Tp ? (i0 >> 1) : 0);
-    y0v[q] = ld(ry, e0);
-    y1v[q] = ld(ry, e1);
-    a0v[q] = ld(ra, e0);
-    a1v[q] = ld(ra, e1);
-    gpv[q] = ld(rp0, ep) + ld(rp1, ep);
+    if constexpr (EVEN) {
+      const float2 yv = in_ld2(ry, e0), av = in_ld2(ra, e0);
+      y0v[q] = yv.x;
+      y1v[q] = yv.y;
+      a0v[q] = av.x;
+      a1v[q] = av.y;
+    } else {
+      y0v[q] = in_ld(ry, e0);
+      y1v[q] = in_ld(ry, e1);
+      a0v[q] = in_ld(ra, e0);
+      a1v[q] = in_ld(ra, e1);
+    }
+    gpv[q] = in_ld(rp0, ep) + in_ld(rp1, ep);
   }
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
@@ -183,15 +216,22 @@ __global__ __launch_bounds__(256) void in_bwd_kernel(const float* __restrict__ y
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     int i0 = 2 * lane + 2 * G * q;
-    if (i0 < T) {
-      const float v = r * (g0[q] - s1 - z0[q] * s2);
-      dr[i0] = v;
-      rs += v;
-    }
-    if (i0 + 1 < T) {
-      const float v = r * (g1[q] - s1 - z1[q] * s2);
-      dr[i0 + 1] = v;
-      rs += v;
+    const float v0 = r * (g0[q] - s1 - z0[q] * s2), v1 = r * (g1[q] - s1 - z1[q] * s2);
+    if constexpr (EVEN) {
+      if (i0 < T) {
+        *reinterpret_cast<float2*>(dr + i0) = make_float2(v0, v1);
+        rs += v0;
+        rs += v1;
+      }
+    } else {
+      if (i0 < T) {
+        dr[i0] = v0;
+        rs += v0;
+      }
+      if (i0 + 1 < T) {
+        dr[i0 + 1] = v1;
+        rs += v1;
+      }
     }
   }
   if (rowsum) {
@@ -527,12 +567,18 @@ extern "C" {
 int mst_instnorm_lrelu_fwd_f32(const float* y, int64_t rows, int32_t T, float eps, float slope,
                                float* a, float* pooled, float* mean, float* rstd, void* stream) {
   MST_REQUIRE(y && a && mean && rstd && rows > 0 && T > 1);
+  MST_REQUIRE(rows * (long long)T < (1ll << 29));  // 32-bit buffer byte offsets in in_fwd_kernel
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
   const int g = in_lanes(T);
   dim3 gs((unsigned)((rows * g + 255) / 256));
-#define MST_IN(NP_, G_, GR) hipLaunchKernelGGL((in_fwd_kernel<NP_, G_>), GR, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd)
+  const bool even = T % 2 == 0 && (((uintptr_t)y | (uintptr_t)a) & 7) == 0;
+#define MST_IN(NP_, G_, GR)                                                                            \
+  do {                                                                                                 \
+    if (even) hipLaunchKernelGGL((in_fwd_kernel<NP_, G_, true>), GR, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd); \
+    else hipLaunchKernelGGL((in_fwd_kernel<NP_, G_, false>), GR, block, 0, st, y, rows, T, eps, slope, a, pooled, mean, rstd); \
+  } while (0)
   if (np <= 1 && g < 64) {
     if (g == 4) MST_IN(1, 4, gs);
     else if (g == 8) MST_IN(1, 8, gs);
@@ -558,7 +604,12 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
   int np = (T + 127) / 128;
   const int g = in_lanes(T);
   dim3 gs((unsigned)((rows * g + 255) / 256));
-#define MST_IN(NP_, G_, GR) hipLaunchKernelGGL((in_bwd_kernel<NP_, G_>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum)
+  const bool even = T % 2 == 0 && (((uintptr_t)y | (uintptr_t)d_a | (uintptr_t)dy) & 7) == 0;
+#define MST_IN(NP_, G_, GR)                                                                            \
+  do {                                                                                                 \
+    if (even) hipLaunchKernelGGL((in_bwd_kernel<NP_, G_, true>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum); \
+    else hipLaunchKernelGGL((in_bwd_kernel<NP_, G_, false>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum); \
+  } while (0)
   if (np <= 1 && g < 64) {
     if (g == 4) MST_IN(1, 4, gs);
     else if (g == 8) MST_IN(1, 8, gs);
