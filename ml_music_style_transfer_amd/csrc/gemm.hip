@@ -626,6 +626,12 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
 // 256-thread groups g: group g loads A units 2g, 2g+1 and the B half n0 + 128 g (all 4 units), so
 // the per-thread loader is the 128 x 128 kernel's with 6 units instead of 8.
 constexpr int BNW = 256, NTHRW = 512;
+#ifndef MST_W_VPM
+#define MST_W_VPM 3  // split VALU placed per MFMA (sweep)
+#endif
+#ifndef MST_W_DSE
+#define MST_W_DSE 4  // one LDS store per MST_W_DSE MFMAs (sweep)
+#endif
 constexpr int PLANE_BW = BNW * LDKB;              // bf16 elements per B plane (256 rows)
 constexpr int STAGE_BF = 3 * PLANE + 3 * PLANE_BW;  // bf16 elements per stage (72 KB)
 constexpr int LDS_W_FLOATS = STAGE_BF;            // two stages = 144 KB; the 128 KB epilogue tile aliases
@@ -777,8 +783,8 @@ __device__ __forceinline__ void tile_pass_w(const GP& p, float* lds, int m_t, in
       for (int i = 0; i < 48; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
         if (i < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU (split)
-        if (i % 4 == 3) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+        __builtin_amdgcn_sched_group_barrier(0x002, MST_W_VPM, 0);        // VALU (split)
+        if (i % MST_W_DSE == MST_W_DSE - 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
       }
       __syncthreads();
     };
