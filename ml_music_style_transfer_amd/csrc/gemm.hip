@@ -626,11 +626,16 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
 // 256-thread groups g: group g loads A units 2g, 2g+1 and the B half n0 + 128 g (all 4 units), so
 // the per-thread loader is the 128 x 128 kernel's with 6 units instead of 8.
 constexpr int BNW = 256, NTHRW = 512;
+// Interleave of the split with the MFMAs (sched_group_barrier): MST_W_VPM split VALU per MFMA
+// and one LDS store per MST_W_DSE MFMAs, so the 12 plane stores of a K tile land in its first
+// 24 MFMA slots. Swept on gemm_micro and the step (profiles/r04/gemm_micro_m11_*, m12_*): one
+// store per 4 MFMAs (the first version) 148.5 TF/s for a T = 252 conv fwd, per 2: 156.7-158.8,
+// per 1: 157.1-157.4, per 6: 138.8; 2 or 4 VALU per MFMA were no better than 3.
 #ifndef MST_W_VPM
-#define MST_W_VPM 3  // split VALU placed per MFMA (sweep)
+#define MST_W_VPM 3
 #endif
 #ifndef MST_W_DSE
-#define MST_W_DSE 4  // one LDS store per MST_W_DSE MFMAs (sweep)
+#define MST_W_DSE 2
 #endif
 constexpr int PLANE_BW = BNW * LDKB;              // bf16 elements per B plane (256 rows)
 constexpr int STAGE_BF = 3 * PLANE + 3 * PLANE_BW;  // bf16 elements per stage (72 KB)
