@@ -536,17 +536,18 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
       load_tile(S, kt + 2, tap, blk);
       advance();
       mfma_tile();
-      // Interleave the next-tile global loads with this tile's MFMAs, one load per two MFMAs
-      // (sched_group_barrier). Issued as a block above the MFMAs they cost 15-25 % of the
+      // Interleave the next-tile global loads with this tile's MFMAs, spread evenly over the 48
+      // MFMAs (sched_group_barrier). Issued as a block above the MFMAs they cost 15-25 % of the
       // GEMM (A/B: conv fwd +5-10 %, dgrad +9-13 %, wgrad +15-25 %); left to the scheduler
-      // they sink next to their wait.
+      // they sink next to their wait. Evenly spread instead of one per MFMA from the first
+      // (round 4): wgrad +1.5-2.4 % (gemm_micro), the step +0.6 % (profiles/r04/
+      // gemm_micro_m14_*); s_setprio 1 around the MFMAs lost 8 %.
       constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
       constexpr int NMF = 48;                                   // MFMAs per tile per wave
-      constexpr int PER = NMF / NV > 2 ? 2 : (NMF / NV < 1 ? 1 : NMF / NV);
 #pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);  // VMEM read
-        __builtin_amdgcn_sched_group_barrier(0x8, PER, 0); // MFMA
+      for (int i = 0; i < NMF; ++i) {
+        if ((i + 1) * NV / NMF != i * NV / NMF) __builtin_amdgcn_sched_group_barrier(0x20, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);  // MFMA
       }
       __syncthreads();  // one buffer: its MFMA reads first
       store_tile(std::integral_constant<int, sb ^ 1>{});
@@ -787,7 +788,10 @@ __device__ __forceinline__ void tile_pass_w(const GP& p, float* lds, int m_t, in
 #pragma unroll
       for (int i = 0; i < 48; ++i) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
-        if (i < NV) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // VMEM read
+        // next-tile loads spread evenly over the 48 MFMAs (in the first NV slots before: T = 252
+        // conv fwd 160.7 -> 165.1, dgrad 175.3 -> 180.8 TF/s, T = 15 +6-8 %, step +2.1 %,
+        // profiles/r04/gemm_micro_m15_*)
+        if ((i + 1) * NV / 48 != i * NV / 48) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, MST_W_VPM, 0);        // VALU (split)
         if (i % MST_W_DSE == MST_W_DSE - 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
       }
