@@ -201,6 +201,7 @@ struct GP {
   // split-K slab
   float* ws;
   int wide;  // conv / dgrad on the 128 x 256 kernel (gemm_w_kernel)
+  int wvec;  // wgrad: dwordx4 loads in unmasked unit-stride K classes (MST_WG_VEC=0: dword)
   // stream-K (sk_L > 0): the grid's G workgroups each run sk_L consecutive iterations of the
   // flattened (tile, 32-deep K tile) space of sk_I = tiles * nk iterations
   long long sk_L, sk_I;
@@ -395,8 +396,9 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
   // padded to a multiple of BK: a 32-deep tile has ONE tap and ONE source, so the tile decode
   // is scalar, the lane's time index is one VGPR per tile, and every element offset is a
   // wave-uniform soffset. Padded channels read through a zero-length descriptor (B = 0).
-  auto load_tile = [&](auto S, int kt, int tap, int blk) __attribute__((always_inline)) {
+  auto load_tile = [&](auto S, int kt, int tap, int blk, auto V) __attribute__((always_inline)) {
     constexpr int st_ = decltype(S)::value;
+    constexpr bool vec = decltype(V)::value;
     (void)kt;
     if constexpr (!WG) {
       const bool s1 = DUAL && blk >= p.nb0;
@@ -442,14 +444,24 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
       // wgrad tile of batch row b = tap at time t0ref + 32 * blk: one scalar soffset per operand
       const int sA = (tap * (int)p.sPb + BK * blk) * 4;
       const int sB = (tap * (int)p.sb0 + p.ta * BK * blk) * 4;
+      if constexpr (vec) {
+        // unmasked class, unit stride: each unit's 4 k are 4 consecutive floats of one row, all
+        // in range (an interior tile lies inside its row), so one dwordx4 per unit (dword-aligned;
+        // a partially out-of-range x4 only occurs in prefetches past the class, never consumed)
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u) ra[st_][u] = ldbs4(rA, vA[u], sA);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ra[st_][u][i] = ldbs(rA, vA[u], sA + 4 * i);
+        for (int u = 0; u < 4; ++u) rb[st_][u] = ldbs4(rX0, vB[u][0], sB);
+      } else {
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rb[st_][u][i] = ldbs(rX0, vB[u][i], sB);
+          for (int i = 0; i < 4; ++i) ra[st_][u][i] = ldbs(rA, vA[u], sA + 4 * i);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rb[st_][u][i] = ldbs(rX0, vB[u][i], sB);
+      }
     }
   };
 
@@ -518,22 +530,23 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
   // run(): one pipelined pass over tiles [kb, ke) starting at scalar decode (tap, blk).
   //   conv : (tap, source block) of a tap-major K
   //   wgrad: (batch row b, tile index j within the class), `per` tiles per row
-  auto run = [&](int kb, int ke, int tap, int blk, int per) __attribute__((always_inline)) {
+  auto run = [&](int kb, int ke, int tap, int blk, int per, auto V) __attribute__((always_inline)) {
+    constexpr bool vec = decltype(V)::value;
     auto advance = [&]() __attribute__((always_inline)) {
       if (++blk == per) {
         blk = 0;
         tap += (WG && p.Tp == 16) ? 2 : 1;
       }
     };
-    load_tile(I0{}, kb, tap, blk);
+    load_tile(I0{}, kb, tap, blk, V);
     advance();
-    load_tile(I1{}, kb + 1, tap, blk);
+    load_tile(I1{}, kb + 1, tap, blk, V);
     advance();
     store_tile(I0{});
     __syncthreads();
     auto step = [&](auto S, int kt) __attribute__((always_inline)) {
       constexpr int sb = decltype(S)::value;
-      load_tile(S, kt + 2, tap, blk);
+      load_tile(S, kt + 2, tap, blk, V);
       advance();
       mfma_tile();
       // Interleave the next-tile global loads with this tile's MFMAs, spread evenly over the 48
@@ -542,7 +555,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
       // they sink next to their wait. Evenly spread instead of one per MFMA from the first
       // (round 4): wgrad +1.5-2.4 % (gemm_micro), the step +0.6 % (profiles/r04/
       // gemm_micro_m14_*); s_setprio 1 around the MFMAs lost 8 %.
-      constexpr int NV = WG ? 32 : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
+      constexpr int NV = WG ? (vec ? 8 : 32) : (AMODE == 1 ? 4 : 16) + 16;  // VMEM loads per tile
       constexpr int NMF = 48;                                   // MFMAs per tile per wave
 #pragma unroll
       for (int i = 0; i < NMF; ++i) {
@@ -561,7 +574,7 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
   if constexpr (!WG) {
     if (kt0 < kt1) {
       const int tap = kt0 / p.nbT;
-      run(kt0, kt1, tap, kt0 - tap * p.nbT, p.nbT);
+      run(kt0, kt1, tap, kt0 - tap * p.nbT, p.nbT, std::false_type{});
     }
   } else {
     // K classes (host-built): tiles [cstart[c], cstart[c+1]) are (b, j) row-major with
@@ -570,10 +583,17 @@ __device__ __forceinline__ void tile_pass(const GP& p, float* lds, int m_t,
       const int kb = max(kt0, p.cstart[c]);
       const int ke = min(kt1, p.cstart[c + 1]);
       if (kb >= ke) continue;
-      wg_class_setup(p.ct0[c], p.cmask[c] != 0);
       const int rel = kb - p.cstart[c];
       const int row = rel / p.ccnt[c];
-      run(kb, ke, (p.Tp == 16 ? 2 : 1) * row, rel - row * p.ccnt[c], p.ccnt[c]);
+      const int r0 = (p.Tp == 16 ? 2 : 1) * row, j0 = rel - row * p.ccnt[c];
+      // the setup inside each branch: the x4 branch keeps only vB[u][0] live
+      if (p.cmask[c] == 0 && p.ta == 1 && p.wvec) {
+        wg_class_setup(p.ct0[c], false);
+        run(kb, ke, r0, j0, p.ccnt[c], std::true_type{});
+      } else {
+        wg_class_setup(p.ct0[c], p.cmask[c] != 0);
+        run(kb, ke, r0, j0, p.ccnt[c], std::false_type{});
+      }
     }
   }
 
@@ -849,6 +869,14 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_w_kernel(const GP p) {
 static int gemm_wide() {  // conv / dgrad on the 128 x 256 kernel; MST_GEMM_WIDE=0: the 128 x 128 one
   static const int v = [] {
     const char* e = getenv("MST_GEMM_WIDE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+static int wg_vec() {
+  static const int v = [] {
+    const char* e = getenv("MST_WG_VEC");
     return (e && e[0] == '0') ? 0 : 1;
   }();
   return v;
@@ -1292,6 +1320,7 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   MST_REQUIRE(p.N < (1 << 22));
   p.scale = d->scale;
   p.accumulate = d->accumulate;
+  p.wvec = wg_vec();
   choose_sched(p, d->splitk);
   return MST_OK;
 }
