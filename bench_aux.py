@@ -180,11 +180,29 @@ def _cpu_front(job):
             else SR.melspec(clip, bench.SR, 2048, bench.HOP)).shape
 
 
-def _cpu_parallel_rate(name, clips):
-    """SURVEY 8(d): NumPy's FFT is single-threaded, so the n-way CPU number is a process pool
-    (spawned workers, no GPU state) over the clips; pool start-up is outside the timing."""
+def _cpu_gl(job):
+    """One clip x n_iter Griffin-Lim iterations through the oracle (spawned worker, NumPy only)."""
+    from oracle import spectral_ref as SR
+    clip, n_iter = job
+    Sn = np.abs(SR.stft(clip, 2048, bench.HOP, out_dtype=None))
+    SR.griffinlim(Sn, n_iter=n_iter, hop=bench.HOP, angles=np.ones_like(Sn, dtype=np.complex128))
+    return n_iter
+
+
+def _cpu_mss(job):
+    """One clip pair's multi-scale loss + gradient through the oracle (spawned worker)."""
+    from oracle import spectral_ref as SR
+    p, t, sizes = job
+    SR.multiscale_spectral_loss_grad(p, t, 1.0, 1e-7, sizes)
+    return 1
+
+
+def _pool_rate(fn, jobs, warm):
+    """Jobs per second over a process pool of the job's CPU allotment (bench.cpu_share; spawned
+    workers, one BLAS thread each, no GPU state); pool start-up and a warm-up job per worker are
+    outside the timing. Returns (jobs/s, workers)."""
     import multiprocessing as mp
-    procs = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "16")), os.cpu_count() or 1))
+    procs = bench.cpu_share()
     keys = ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")
     saved = {k: os.environ.get(k) for k in keys}
     os.environ.update({k: "1" for k in keys})  # one BLAS thread per worker: no oversubscription
@@ -197,11 +215,18 @@ def _cpu_parallel_rate(name, clips):
             else:
                 os.environ[k] = v
     with pool:
-        pool.map(_cpu_front, [(name, clips[0])] * procs)  # warm every worker
+        pool.map(fn, [warm] * procs)  # warm every worker
         t0 = time.perf_counter()
-        pool.map(_cpu_front, [(name, c) for c in clips], chunksize=max(1, len(clips) // (4 * procs)))
+        pool.map(fn, jobs, chunksize=max(1, len(jobs) // (4 * procs)))
         dt = time.perf_counter() - t0
-    return {"value": round(len(clips) / dt, 2), "cores": procs,
+    return len(jobs) / dt, procs
+
+
+def _cpu_parallel_rate(name, clips):
+    """SURVEY 8(d): NumPy's FFT is single-threaded, so the n-way CPU number is a process pool
+    (spawned workers, no GPU state) over the clips; pool start-up is outside the timing."""
+    rate, procs = _pool_rate(_cpu_front, [(name, c) for c in clips], (name, clips[0]))
+    return {"value": round(rate, 2), "cores": procs,
             "sample": f"{len(clips)} clips, multiprocessing pool of {procs} spawned workers"}
 
 
@@ -326,6 +351,14 @@ def griffinlim(args, world, rank, dev):
         cpu = {"value": round(1.0 / (c * n_iter), 3), "unit": "clips/s (60 iterations)", "cores": 1,
                "kind": "port", "sample": "1 clip x 10 iterations of oracle/spectral_ref.griffinlim "
                                          "(NumPy float64, 1 thread), scaled to 60 iterations"}
+        if getattr(args, "parallel_cpu", True):
+            try:
+                rate, procs = _pool_rate(_cpu_gl, [(x[i], 10) for i in range(bench.cpu_share())], (x[0], 1))
+                cpu["parallel"] = {"value": round(rate * 10 / n_iter, 3), "cores": procs,
+                                   "sample": f"{procs} clips x 10 iterations, multiprocessing pool of "
+                                             f"{procs} spawned workers, scaled to 60 iterations"}
+            except Exception as e:  # a baseline leg must not cost the measured line
+                cpu["parallel"] = {"error": repr(e)[:200]}
     extra = {"kernel_ms": round(kms, 3)}
     if rank == 0 and not args.no_parity:
         extra["parity"] = _gl_parity(S, fn(), [0, B - 1], n_iter, args)
@@ -336,9 +369,6 @@ def griffinlim(args, world, rank, dev):
                   _roof(B * n_iter * bpi / (kms * 1e-3) / 1e9,
                         "gl_synth_kernel (atomic seams) + stft_fm_kernel<COMPLEX> per iteration",
                         B * n_iter * bpi, traffic=_gl_traffic(n_iter)), cpu, extra)]
-
-
-MSS_SILENT_TOL = 2e-3  # targets with exact silence (see mss())
 
 
 def _torch_fp32_mss_gap(p, t, sizes, ref):
@@ -383,6 +413,17 @@ def mss(args, world, rank, dev):
         cpu = {"value": round(1.0 / c, 3), "unit": "clip-pairs/s", "cores": 1, "kind": "port",
                "sample": "1 clip pair (10 s @ 22.05 kHz), loss + gradient by "
                          "oracle/spectral_ref.multiscale_spectral_loss_grad (NumPy float64)"}
+        if getattr(args, "parallel_cpu", True):
+            try:
+                pr = pred.detach().cpu().double().numpy()
+                tg = tgt.cpu().double().numpy()
+                n = min(B, bench.cpu_share())
+                rate, procs = _pool_rate(_cpu_mss, [(pr[i], tg[i], list(sizes)) for i in range(n)],
+                                         (pr[0, :8192], tg[0, :8192], list(sizes)))
+                cpu["parallel"] = {"value": round(rate, 3), "cores": procs,
+                                   "sample": f"{n} clip pairs, multiprocessing pool of {procs} spawned workers"}
+            except Exception as e:  # a baseline leg must not cost the measured line
+                cpu["parallel"] = {"error": repr(e)[:200]}
     extra = {"kernel_ms": round(kms, 4), "approx_fft_gflop_per_step": round(B * flops / 1e9, 2)}
     if rank == 0 and not args.no_parity:
         p0 = pred.detach()[:1].clone().requires_grad_(True)
@@ -390,29 +431,31 @@ def mss(args, world, rank, dev):
         ref, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
                                                   tgt[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
         rel = abs(l0.item() - ref) / abs(ref)
-        # Fixed bars per input class. The piano target of pair 0 has exact silence (11 % of its
-        # samples) and bins far below fp32 resolution, which log(S + 1e-7) amplifies: torch's own
-        # fp32 path misses float64 by 1.2e-3 on it (reported as a diagnostic), so that class gets
-        # MSS_SILENT_TOL. The same pair with the silence filled by low-level noise is the
-        # non-silent class and must meet north_star's 1e-4.
+        # north_star's 1e-4 on both input classes. The piano target of pair 0 has exact silence
+        # (11 % of its samples) and bins far below fp32 resolution, which log(S + 1e-7)
+        # amplifies: torch's own fp32 path misses float64 by 1.2e-3 on it (reported as a
+        # diagnostic); the target transform here runs in float64 (mss_target_kernel). The same
+        # pair with the silence filled by low-level noise is the non-silent class.
         gap = _torch_fp32_mss_gap(p0.detach()[0].cpu().numpy(), tgt[0].cpu().numpy(), sizes, ref)
         t1 = tgt[:1] + 1e-3 * torch.from_numpy(rng.standard_normal((1, L)).astype(np.float32)).to(dev)
         l1 = spectral.multiscale_spectral_loss(p0.detach(), t1, sizes=sizes)
         ref1, _ = SR.multiscale_spectral_loss_grad(p0.detach()[0].cpu().double().numpy(),
                                                    t1[0].cpu().double().numpy(), 1.0, 1e-7, sizes)
         rel1 = abs(l1.item() - ref1) / abs(ref1)
-        ok = rel <= MSS_SILENT_TOL and rel1 <= 1e-4
+        ok = rel <= 1e-4 and rel1 <= 1e-4
         extra["parity"] = {"pair": 0, "loss": l0.item(), "oracle": ref, "rel_err": rel,
-                           "tol": MSS_SILENT_TOL, "torch_fp32_rel_err": gap,
+                           "tol": 1e-4, "torch_fp32_rel_err": gap,
                            "nonsilent": {"loss": l1.item(), "oracle": ref1, "rel_err": rel1, "tol": 1e-4},
-                           **_verdict(ok, f"multi-scale loss of pair 0: rel {rel:.2e} (bar {MSS_SILENT_TOL:.0e}),"
+                           **_verdict(ok, f"multi-scale loss of pair 0: rel {rel:.2e} (bar 1e-4),"
                                           f" non-silent rel {rel1:.2e} (bar 1e-4)", args)}
     return [_line("multi-scale spectral loss fwd+grad clip-pairs/s, 10 s @ 22.05 kHz, 6 FFT sizes",
                   world * B / dt, "clip-pairs/s", world, args.steps, args.warmup, dt * 1e3,
                   {"workload": "config 5: DDSP multi-scale spectral loss + d/d pred",
                    "pairs_per_gpu": B, "L": L, "sizes": list(sizes)},
                   _roof(B * bpp / (kms * 1e-3) / 1e9,
-                        "mss_multi_kernel (n = 64..1024 in one launch), mss_fft2048_kernel, ordered slab sum + fold + loss reduce (pred and target each a real FFT)",
+                        "mss_target_kernel (float64 target magnitudes, every size in one launch), "
+                        "mss_multi_kernel (n = 64..1024 in one launch), mss_fft2048_kernel, ordered "
+                        "slab sum + fold + loss reduce",
                         B * bpp, traffic=_mss_traffic()), cpu, extra)]
 
 

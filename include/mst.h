@@ -28,6 +28,9 @@
  *   mst_adam_f32 / _ex_f32 / _dev_f32
  *                            model/train.py:188,143             optim.Adam(lr=1e-3)
  *   mst_onoff_f32            preprocessing/preprocess.py:148-155 piano-roll binarise + onset/offset
+ *   mst_render_logpow_f32 / _bwd_f32
+ *                            model/inference.py:109 sqrt(expm1(clip(S,0,20))) with a held phase:
+ *                            the multi-scale loss as a training loss (README.md:23, train.py:119-123)
  */
 #ifndef MST_H
 #define MST_H
@@ -229,6 +232,16 @@ size_t mst_mss_workspace_size(int64_t B, int64_t L, int32_t n_sizes, const int32
 int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t L, int32_t n_sizes,
                      const int32_t* sizes, float alpha, float eps, float* loss, float* dpred,
                      void* workspace, size_t ws_bytes, void* stream);
+
+/* ---- log-power spectrogram -> complex spectrum with a held phase (the multi-scale loss as a
+ * training loss; inference.py:109's magnitude inversion):
+ *   X[b][t][f] = sqrt(expm1(clip(S[b][f][t], 0, 20))) * P[b][t][f] / |P[b][t][f]|  (1 if |P| = 0)
+ * S (B, F, T) log-power; P, X (B, T, F, 2) frame-major complex (mst_stft_complex_f32's layout).
+ * _bwd: dS[b][f][t] = Re(conj(U) dX[b][t][f]) * e^S / (2 M) inside (0, 20), else 0. ---- */
+int mst_render_logpow_f32(const float* S, const float* P, int32_t B, int32_t F, int32_t T, float* X,
+                          void* stream);
+int mst_render_logpow_bwd_f32(const float* S, const float* P, const float* dX, int32_t B, int32_t F,
+                              int32_t T, float* dS, void* stream);
 
 /* ---- piano roll (preprocess.py:148-155): roll (B, T, 128) velocities ->
  *      binarised roll and onoff, both (B, T, 128) ---- */

@@ -99,6 +99,10 @@ SIGNATURES = {
                                    c_void_p, c_float, c_float, c_void_p, c_void_p, c_void_p,
                                    c_size_t, c_void_p]),
     "mst_onoff_f32": (c_int32, [c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p]),
+    "mst_render_logpow_f32": (c_int32, [c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                        c_void_p]),
+    "mst_render_logpow_bwd_f32": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32,
+                                            c_void_p, c_void_p]),
     "mst_version": (ctypes.c_char_p, []),
     "mst_gemm_products": (c_int32, []),
     "mst_device_arch": (c_int32, [ctypes.c_char_p, c_int32]),

@@ -1686,10 +1686,9 @@ __device__ __forceinline__ int mss_reflect(int i, int L) {
 // lane 64 - l, register 15 - j (lane 0 keeps its own). Frames a and b of a pair then sit in the
 // wave's LDS buffer as (g_a, g_b) for the workgroup's ordered overlap-add. Three fft1024_v2 per
 // frame, as in the packed form this replaces.
-__device__ __forceinline__ c2 mss_term(c2 P, c2 Q, bool use, bool own, bool grad, const MssArgs& a,
+__device__ __forceinline__ c2 mss_term(c2 P, float st, bool use, bool own, bool grad, const MssArgs& a,
                                        float& s_abs, float& s_log) {
   const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
-  const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
   c2 g2 = mk(0.f, 0.f);
   if (use) {
     if (own) {
@@ -1733,7 +1732,7 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = (int)a.L;
   const float* p = a.pred + (long long)b * a.L;
-  const float* q = a.target + (long long)b * a.L;
+  const float* tm = a.tmag + (long long)b * a.T * (HALF + 1);  // float64-accurate |X_target|
   const bool grad = a.dpred != nullptr;
   {
     const float4* src = reinterpret_cast<const float4*>(&kFftTabs);
@@ -1769,32 +1768,40 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
       for (int pass = 0; pass < 2; ++pass) {
         const int t = t_base + pass;
         const bool valid = t < f_own1;
-        c2 vp[16], vq[16];
+        // the target's magnitudes at bins k = l + 64 j, 1024 - k and 512, loaded ahead of the FFT
+        // (clamped frame: a past-the-end frame reads a valid row and is masked by `valid`)
+        const float* tr = tm + (long long)min(t, a.T - 1) * (HALF + 1);
+        float qk[8], qm[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          qk[j] = tr[lane + 64 * j];
+          qm[j] = tr[HALF - lane - 64 * j];
+        }
+        const float q512 = tr[512];
+        c2 vp[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int n = lane + 64 * j;
-          vp[j] = vq[j] = mk(0.f, 0.f);
+          vp[j] = mk(0.f, 0.f);
           if (valid) {
             const int s0 = t * H + 2 * n - HALF;
             const int i0 = mss_reflect(s0, L), i1 = mss_reflect(s0 + 1, L);
             const float h0 = hann(2 * n), h1 = hann(2 * n + 1);
             vp[j] = mk(h0 * p[i0], h1 * p[i1]);
-            vq[j] = mk(h0 * q[i0], h1 * q[i1]);
           }
         }
         fft1024_v2(vp, S, tb, lane);  // Z_pred[l + 64 j]
-        fft1024_v2(vq, S, tb, lane);  // Z_target[l + 64 j]
         const bool own = t >= f_own0;
-        c2 pk[8], pm[8], qk[8], qm[8], yk[8], ym[8];
+        c2 pk[8], pm[8], yk[8], ym[8];
         real_pairs(vp, tb, lane, src, pk, pm);
-        real_pairs(vq, tb, lane, src, qk, qm);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           yk[j] = mss_term(pk[j], qk[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
+          // lane 0's X[1024 - 0] is the Nyquist bin X[1024] (xm[0]), its magnitude tr[1024]
           ym[j] = mss_term(pm[j], qm[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
         }
         // f = 512: X[512] = conj Z[512] (lane 0, register 8)
-        const c2 y512 = mss_term(conj(vp[8]), conj(vq[8]), valid && lane == 0, own, grad, a, s_abs, s_log) * 0.5f;
+        const c2 y512 = mss_term(conj(vp[8]), q512, valid && lane == 0, own, grad, a, s_abs, s_log) * 0.5f;
         if (!grad) continue;
         if (lane == 0) {  // Y_0, Y_1024 are real (and G_f / 2 -> G_f there)
           yk[0] = mk(2.f * yk[0].x, 0.f);
@@ -1874,22 +1881,15 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   float* dp = a.dpred + (long long)b * a.L;
   float* ed = a.edges + (long long)b * N;
   const int own_hi = min(own_lo + MSS_RWIN, L + N);
-  // the previous sizes' sums, loaded together up front (clamped in range; a load inside the
-  // per-sample branch below made hipcc wait for each one: 16 serialised round trips)
-  float prev[OWN];
-#pragma unroll
-  for (int i = 0; i < OWN; ++i)
-    prev[i] = dp[min(max(own_lo + tid + 256 * i - HALF, 0), L - 1)];  // unconditional: no join
+  // this size's gradient slab (the sizes are summed in order by mss_sum_kernel, mss.hip)
 #pragma unroll
   for (int i = 0; i < OWN; ++i) {
     // one store per sample to the address picked by selects (stores under the three-way
     // branch each waited for every earlier store: vmcnt counts stores on gfx950)
     const int pp = own_lo + tid + 256 * i;
     const int x = pp - HALF;
-    const float v0 = acc[i];
     float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
-    const float val = (x >= 0 && x < L && a.accumulate) ? prev[i] + v0 : v0;
-    if (pp < own_hi) *dst = val;
+    if (pp < own_hi) *dst = acc[i];
   }
 }
 

@@ -1014,10 +1014,15 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
   }
 }
 
-// Split-K from a wave-quantisation cost model. 256 CUs x 2 resident workgroups = 512 slots;
-// a workgroup's time is ~ (its K tiles) x tau. A trailing partial wave of <= 256 workgroups
-// runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave. Split-K
-// adds a slab round trip (s + 2 passes over M x N floats at ~5 TB/s) plus a launch.
+// Split-K from a wave-quantisation cost model. 256 CUs x occ resident workgroups = the slots;
+// a workgroup's time is ~ (its K tiles) x tau. At occ = 2 a trailing partial wave of <= 256
+// workgroups runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave;
+// at occ = 1 (the 128 x 256 kernel) a lone workgroup runs no faster than in a full wave, so a
+// partial wave costs a whole one (MST_W_PARTIAL). Split-K adds a slab round trip (s + 2 passes
+// over M x N floats) plus a launch.
+#ifndef MST_W_PARTIAL
+#define MST_W_PARTIAL 1.0
+#endif
 int choose_splitk(int M, int N, int nk, int req, int occ, int bn = BN) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
   const long long tiles = (long long)ceil_div(M, BM) * ceil_div(N, bn);
@@ -1033,7 +1038,7 @@ int choose_splitk(int M, int N, int nk, int req, int occ, int bn = BN) {
   }();
   auto waves = [&](long long n) {
     long long full = n / (long long)slots, rem = n % (long long)slots;
-    return (double)full + (rem == 0 ? 0.0 : (rem <= slots / 2 ? 0.55 : 1.0));
+    return (double)full + (rem == 0 ? 0.0 : (rem <= slots / 2 ? (occ == 1 ? MST_W_PARTIAL : 0.55) : 1.0));
   };
   int best = 1;
   double best_t = waves(tiles) * nk * tau;
@@ -1107,10 +1112,13 @@ int launch(const GP& p, hipStream_t st, int taps) {
   dim3 block(NTHR);
   const bool wide = !WG && p.wide && p.sk_L == 0;
   const dim3 wgrid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk), wblock(NTHRW);
+  // (wide implies !WG: the weight-gradient instantiations never reference gemm_w_kernel)
 #define MST_GEMM_LAUNCH(TP, AM)                                                      \
   if (wide) {                                                                        \
-    if (p.dual) hipLaunchKernelGGL((gemm_w_kernel<TP, AM, true>), wgrid, wblock, 0, st, p); \
-    else hipLaunchKernelGGL((gemm_w_kernel<TP, AM, false>), wgrid, wblock, 0, st, p); \
+    if constexpr (!WG) {                                                             \
+      if (p.dual) hipLaunchKernelGGL((gemm_w_kernel<TP, AM, true>), wgrid, wblock, 0, st, p); \
+      else hipLaunchKernelGGL((gemm_w_kernel<TP, AM, false>), wgrid, wblock, 0, st, p); \
+    }                                                                                \
   } else if (!WG && p.dual)                                                          \
     hipLaunchKernelGGL((gemm_kernel<TP, WG, AM, !WG>), grid, block, 0, st, p);       \
   else                                                                               \

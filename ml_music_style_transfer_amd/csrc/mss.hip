@@ -14,7 +14,8 @@
 // HBM. Every frame of pred and of target is transformed on its own as a real FFT (an n/2-point
 // complex transform of the even/odd samples plus the post-twist), in place inside one wave;
 // the two gradient frames of a frame pair are packed into one Hermitian-completed inverse
-// transform (real part = frame a, imaginary part = frame b).
+// transform (real part = frame a, imaginary part = frame b). The target is transformed once per
+// call, in float64 (mss_target_kernel), and the loss kernels read its magnitudes.
 // Deterministic: fixed summation order everywhere; each size writes its own gradient slab and
 // mss_sum_kernel adds the slabs in size order; reflect-pad edges are folded in by a final kernel.
 #include <cstdlib>
@@ -203,7 +204,7 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int L = (int)a.L;
   const float* p = a.pred + (long long)b * a.L;
-  const float* q = a.target + (long long)b * a.L;
+  const float* tm = a.tmag + (long long)b * a.T * NBIN;  // float64-accurate |X_target| (B, T, NBIN)
   const bool grad = a.dpred != nullptr;
   // twiddles and window from the compile-time W2048 quarter table (N divides 1024): W_N^r =
   // W2048^(r 2048 / N); the periodic Hann in its sin^2 form, sin(pi j / N) = sin(2 pi m / 2048)
@@ -241,37 +242,43 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
       c2 zga[NE], zgb[NE];
 #pragma unroll
       for (int pass = 0; pass < 2; ++pass) {
-        // load + window FB frames t_base + 2m + pass, each signal on its own as an n/2-point
-        // complex transform (transform 2m: pred, 2m + 1: target): z_j = w_2j x_2j + i w_2j+1 x_2j+1.
-        // (Packing pred and target into one complex signal, as before, left the target's
-        // spectrum with rounding noise of the pred's size: exact silence in the target came out
-        // as ~1e-6 and log(S + eps) moved the loss by 0.2-1 %, tools/mss_probe.py.)
+        // the target's magnitudes of this pass's frames, loaded ahead of the FFT (the target is
+        // transformed once, in float64, by mss_target_kernel: an fp32 transform leaves its
+        // near-silent bins at fp32 rounding noise, which log(S + eps) turns into a 1e-3 loss error)
+        float stv[NE];
+#pragma unroll
+        for (int jj = 0; jj < NE; ++jj) {
+          const int e = min(lane + 64 * jj, FB * NBIN - 1), m = e / NBIN, f = e - m * NBIN;
+          const int t = min(t_base + 2 * m + pass, f_own1 - 1);  // clamped: masked below
+          stv[jj] = tm[(long long)t * NBIN + f];
+        }
+        // load + window FB pred frames t_base + 2m + pass, each an n/2-point complex transform
+        // z_j = w_2j x_2j + i w_2j+1 x_2j+1 in the first half of the wave's buffer.
         // Branch-free: a frame past f_own1 loads frame f_own1 - 1 (always in range) and is
         // zeroed by a select; a load under a per-element branch made hipcc wait for each
         // element's loads at the join (32 serialised global round trips per round).
         constexpr int KC = LOG2N >= 10 ? 4 : 8;  // elements per load batch (2 KC loads in flight)
 #pragma unroll
-        for (int k0 = 0; k0 < BW / 64; k0 += KC) {
+        for (int k0 = 0; k0 < BW / 128; k0 += KC) {
           float x0[KC], x1[KC];
 #pragma unroll
           for (int kk = 0; kk < KC; ++kk) {
             const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
-            const int t = min(t_base + 2 * (u >> 1) + pass, f_own1 - 1);
-            const float* x = (u & 1) ? q : p;
+            const int t = min(t_base + 2 * u + pass, f_own1 - 1);
             const int s0 = t * H + 2 * j - HALF;
-            x0[kk] = x[reflect(s0, L)];
-            x1[kk] = x[reflect(s0 + 1, L)];
+            x0[kk] = p[reflect(s0, L)];
+            x1[kk] = p[reflect(s0 + 1, L)];
           }
 #pragma unroll
           for (int kk = 0; kk < KC; ++kk) {
             const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
-            const bool live = t_base + 2 * (u >> 1) + pass < f_own1;
+            const bool live = t_base + 2 * u + pass < f_own1;
             const float2 wj = *reinterpret_cast<const float2*>(hw + 2 * j);
             S[e] = live ? mk(wj.x * x0[kk], wj.y * x1[kk]) : mk(0.f, 0.f);
           }
         }
         wave_sync();
-        wave_fft<LOG2N - 1, BW, false>(S, qth, lane);
+        wave_fft<LOG2N - 1, BW / 2, false>(S, qth, lane);
         // spectra, loss, gradient spectra (registers)
 #pragma unroll
         for (int jj = 0; jj < NE; ++jj) {
@@ -290,10 +297,10 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
               const c2 E = (A + Bc) * 0.5f, D = A - Bc;
               return E + cmul(wf, mk(D.y * 0.5f, -D.x * 0.5f));
             };
-            const c2 P = bin(S + 2 * m * HALF), Q = bin(S + (2 * m + 1) * HALF);
+            const c2 P = bin(S + m * HALF);
             // hardware sqrt / log2 / rcp (1 ulp): the library forms add ~10 instructions each
             const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
-            const float st = __builtin_amdgcn_sqrtf(Q.x * Q.x + Q.y * Q.y);
+            const float st = stv[jj];
             const float lp = __log2f(sp + a.eps) * 0.69314718055994531f;
             const float lt = __log2f(st + a.eps) * 0.69314718055994531f;
             if (t >= f_own0) {
@@ -384,6 +391,192 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
     float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
     if (pp < own_hi) *dst = acc[i];
   }
+}
+
+// ------------------------------------------------------------------ target magnitudes, float64
+// |STFT_n(target)| for every size, frame-major (B, T_n, n/2 + 1), computed in float64 and rounded
+// to float: an fp32 transform leaves bins far below the frame's peak at fp32 rounding noise (a
+// silent or decaying target's high bins), and log(S + 1e-7) turns that noise into a 1e-3 loss
+// error against the float64 definition (bench_aux's silent piano pair). The target needs no
+// gradient, so it is transformed once per call here and the loss kernels read its magnitudes.
+// One wave transforms FBT = BWT / (n/2) frames at a time in its LDS buffer (n/2-point complex
+// Stockham FFT of z_j = w_2j x_2j + i w_2j+1 x_2j+1, then the real-FFT post-twist), twiddles and
+// window from a compile-time float64 W2048 table.
+struct MssW2048d {
+  double2 w[512];
+};
+constexpr MssW2048d make_mss_w2048d() {
+  MssW2048d t{};
+  double c = 0, s = 0;
+  for (int k = 0; k < 512; ++k) {
+    cx_sincos_turn(k, 2048, c, s);
+    t.w[k] = double2{c, -s};
+  }
+  return t;
+}
+__device__ constexpr MssW2048d kMssW2048d = make_mss_w2048d();
+
+struct d2 {
+  double x, y;
+};
+__device__ __forceinline__ d2 dk(double x, double y) { return d2{x, y}; }
+__device__ __forceinline__ d2 operator+(d2 a, d2 b) { return dk(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ d2 operator-(d2 a, d2 b) { return dk(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ d2 dmul(d2 a, d2 b) { return dk(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x); }
+
+// W_N^m (N | 2048) from the quarter table: W2048^(m 2048 / N) = (-i)^q W2048^r
+__device__ __forceinline__ d2 twd(const d2* qt, int m, int N) {
+  const int k = (m & (N - 1)) * (2048 / N), q = k >> 9, r = k & 511;
+  const d2 w = qt[r];
+  const bool odd = q & 1, neg = q & 2;
+  const double a = odd ? w.y : w.x, b = odd ? -w.x : w.y;
+  return dk(neg ? -a : a, neg ? -b : b);
+}
+
+// FB transforms of size N = 2^LOG2N in place in s[0 .. FB N) (Stockham, natural-order result)
+template <int LOG2N, int BWT>
+__device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
+  constexpr int N = 1 << LOG2N, NR = N / 4, IT = BWT / 4 / 64;
+  int Ns = 1;
+#pragma unroll
+  for (int st = 0; st < LOG2N / 2; ++st) {
+    d2 v[IT][4];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[it][r] = s[fr * N + j + r * NR];
+    }
+    wave_sync();
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
+      const int k = j & (Ns - 1);
+      if (st > 0) {
+        const d2 w1 = twd(qt, k, 4 * Ns), w2 = dmul(w1, w1), w3 = dmul(w2, w1);
+        v[it][1] = dmul(v[it][1], w1);
+        v[it][2] = dmul(v[it][2], w2);
+        v[it][3] = dmul(v[it][3], w3);
+      }
+      const d2 t0 = v[it][0] + v[it][2], t1 = v[it][0] - v[it][2];
+      const d2 t2 = v[it][1] + v[it][3], t3 = v[it][1] - v[it][3];
+      const d2 it3 = dk(-t3.y, t3.x);
+      d2* d = s + fr * N + (j - k) * 4 + k;
+      d[0] = t0 + t2;
+      d[Ns] = t1 - it3;
+      d[2 * Ns] = t0 - t2;
+      d[3 * Ns] = t1 + it3;
+    }
+    wave_sync();
+    Ns *= 4;
+  }
+  if constexpr (LOG2N & 1) {
+    constexpr int NR2 = N / 2, IT2 = BWT / 2 / 64;
+    d2 v[IT2][2];
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
+      v[it][0] = s[fr * N + j];
+      v[it][1] = s[fr * N + j + NR2];
+    }
+    wave_sync();
+#pragma unroll
+    for (int it = 0; it < IT2; ++it) {
+      const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
+      const int k = j & (Ns - 1);
+      const d2 b = dmul(v[it][1], twd(qt, k, 2 * Ns));
+      d2* d = s + fr * N + (j - k) * 2 + k;
+      d[0] = v[it][0] + b;
+      d[Ns] = v[it][0] - b;
+    }
+    wave_sync();
+  }
+}
+
+constexpr int MSS_TW = 4;           // waves per target workgroup
+constexpr int MSS_TBW = 512;        // complex doubles per wave buffer (n/2 <= 512); n = 2048: 1024
+constexpr int MSS_TROUNDS = 4;      // frame batches per wave per workgroup
+constexpr int MSS_TLDS = MSS_TW * 1024 * 16 + 512 * 16;  // wave buffers (n = 2048 size) + table
+
+struct MssTgt {
+  const float* target;
+  long long L;
+  int nsz;
+  int lg[8], T[8], nblk[8];
+  float* tmag[8];
+};
+
+template <int LOG2N>
+__device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk, int b, char* lds) {
+  constexpr int N = 1 << LOG2N, H = N / 4, HALF = N / 2, NBIN = HALF + 1;
+  constexpr int BWT = HALF > MSS_TBW ? HALF : MSS_TBW;
+  constexpr int FBT = BWT / HALF;            // frames per wave batch
+  constexpr int NEO = (FBT * NBIN + 63) / 64;  // output bins per lane
+  d2* qt = reinterpret_cast<d2*>(lds);
+  d2* S = qt + 512 + (threadIdx.x >> 6) * 1024;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int r = threadIdx.x; r < 512; r += 256) {
+    const double2 w = kMssW2048d.w[r];
+    qt[r] = dk(w.x, w.y);
+  }
+  __syncthreads();
+  const int L = (int)A.L, T = A.T[z];
+  const float* x = A.target + (long long)b * A.L;
+  float* out = A.tmag[z] + (long long)b * T * NBIN;
+  constexpr int PER_WG = MSS_TW * FBT * MSS_TROUNDS;
+#pragma unroll 1
+  for (int rd = 0; rd < MSS_TROUNDS; ++rd) {
+    const int t0 = blk * PER_WG + (rd * MSS_TW + wave) * FBT;  // this wave's first frame
+    if (t0 >= T) break;                                        // wave-uniform
+    // load + window: z_j = w_2j x_2j + i w_2j+1 x_2j+1 (periodic Hann in float64, reflect pad)
+#pragma unroll 4
+    for (int e = lane; e < FBT * HALF; e += 64) {
+      const int u = e / HALF, j = e - u * HALF;
+      const int t = min(t0 + u, T - 1);
+      const int s0 = t * H + 2 * j - HALF;
+      const d2 c0 = twd(qt, 2 * j, N), c1 = twd(qt, 2 * j + 1, N);  // W_N^k: cos(2 pi k / N)
+      const double w0 = 0.5 - 0.5 * c0.x, w1 = 0.5 - 0.5 * c1.x;
+      S[e] = dk(w0 * (double)x[reflect(s0, L)], w1 * (double)x[reflect(s0 + 1, L)]);
+    }
+    wave_sync();
+    wave_fft_d<LOG2N - 1, BWT>(S, qt, lane);
+    // post-twist X_f = E + W_N^f O, E = (Z_f + conj Z_(n/2-f)) / 2, O = -i (Z_f - conj Z_(n/2-f)) / 2
+#pragma unroll
+    for (int jj = 0; jj < NEO; ++jj) {
+      const int e = lane + 64 * jj, m = e / NBIN, f = e - m * NBIN;
+      const int t = t0 + m;
+      if (e < FBT * NBIN && t < T) {
+        const d2* Z = S + m * HALF;
+        const d2 Af = Z[f & (HALF - 1)], Bf = Z[(HALF - f) & (HALF - 1)];
+        const d2 E = dk(0.5 * (Af.x + Bf.x), 0.5 * (Af.y - Bf.y));
+        const d2 D = dk(0.5 * (Af.y + Bf.y), -0.5 * (Af.x - Bf.x));  // -i (A - conj B) / 2
+        const d2 X = E + dmul(twd(qt, f, N), D);
+        out[(long long)t * NBIN + f] = (float)sqrt(X.x * X.x + X.y * X.y);
+      }
+    }
+    wave_sync();  // the spectra are read before the next batch overwrites the buffer
+  }
+}
+
+// grid (max nblk, B, sizes); every size of the call in one launch
+__global__ __launch_bounds__(256, 2) void mss_target_kernel(const MssTgt A) {
+  __shared__ __attribute__((aligned(16))) char lds[MSS_TLDS];
+  const int z = blockIdx.z, blk = blockIdx.x, b = blockIdx.y;
+  if (blk >= A.nblk[z]) return;
+  switch (A.lg[z]) {
+    case 6: mss_target_body<6>(A, z, blk, b, lds); break;
+    case 7: mss_target_body<7>(A, z, blk, b, lds); break;
+    case 8: mss_target_body<8>(A, z, blk, b, lds); break;
+    case 9: mss_target_body<9>(A, z, blk, b, lds); break;
+    case 10: mss_target_body<10>(A, z, blk, b, lds); break;
+    default: mss_target_body<11>(A, z, blk, b, lds); break;
+  }
+}
+
+int mss_target_frames_per_wg(int lg) {
+  const int half = 1 << (lg - 1);
+  const int bwt = half > MSS_TBW ? half : MSS_TBW;
+  return MSS_TW * (bwt / half) * MSS_TROUNDS;
 }
 
 // Sizes n = 64 .. 1024 of one loss call in ONE launch: blockIdx.z picks the size (its workgroups
@@ -539,7 +732,7 @@ int log2i(int n) {
 struct Plan {
   int nsz;
   int n[8], T[8], nwg[8];
-  long long part_off[8], edge_off[8], slab_off[8], slab_stride;
+  long long part_off[8], edge_off[8], slab_off[8], slab_stride, tmag_off[8];
   size_t bytes;
 };
 
@@ -563,7 +756,13 @@ int make_plan(int64_t B, int64_t L, int32_t n_sizes, const int32_t* sizes, Plan&
   pl.slab_stride = (B * L + 3) / 4 * 4;
   const long long slab0 = (part + edge + 3) / 4 * 4;
   for (int s = 0; s < n_sizes; ++s) pl.slab_off[s] = slab0 + s * pl.slab_stride;
-  pl.bytes = (size_t)(slab0 + n_sizes * pl.slab_stride) * sizeof(float);
+  // the target's float64-accurate magnitudes per size (B, T_n, n/2 + 1), 16-byte aligned
+  long long tm = slab0 + n_sizes * pl.slab_stride;
+  for (int s = 0; s < n_sizes; ++s) {
+    pl.tmag_off[s] = tm;
+    tm += (B * pl.T[s] * (pl.n[s] / 2 + 1) + 3) / 4 * 4;
+  }
+  pl.bytes = (size_t)tm * sizeof(float);
   for (int s = 0; s < n_sizes; ++s) pl.edge_off[s] += part;
   return 0;
 }
@@ -588,6 +787,21 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
   hipStream_t st = (hipStream_t)stream;
   float* w = (float*)ws;
   MST_REQUIRE(((uintptr_t)ws & 15) == 0);
+  // the target's magnitudes, every size in one launch
+  MssTgt tg;
+  tg.target = target;
+  tg.L = L;
+  tg.nsz = pl.nsz;
+  unsigned max_blk = 0;
+  for (int s = 0; s < pl.nsz; ++s) {
+    tg.lg[s] = log2i(pl.n[s]);
+    tg.T[s] = pl.T[s];
+    tg.nblk[s] = ceil_div(pl.T[s], mss_target_frames_per_wg(tg.lg[s]));
+    tg.tmag[s] = w + pl.tmag_off[s];
+    max_blk = max_blk > (unsigned)tg.nblk[s] ? max_blk : (unsigned)tg.nblk[s];
+  }
+  hipLaunchKernelGGL(mss_target_kernel, dim3(max_blk, (unsigned)B, (unsigned)pl.nsz), dim3(256), 0, st, tg);
+  MST_CHECK_LAUNCH();
   MssMulti mm;
   mm.nsz = 0;
   unsigned max_nwg = 0;
@@ -595,6 +809,7 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     MssArgs a;
     a.pred = pred;
     a.target = target;
+    a.tmag = w + pl.tmag_off[s];
     a.L = L;
     a.T = pl.T[s];
     a.nwg = pl.nwg[s];
@@ -602,7 +817,6 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     a.eps = eps;
     a.inv_cnt = (float)(1.0 / ((double)B * pl.T[s] * (pl.n[s] / 2 + 1)));
     a.dpred = dpred ? w + pl.slab_off[s] : nullptr;  // this size's slab
-    a.accumulate = 0;
     a.edges = w + pl.edge_off[s];
     a.partial = w + pl.part_off[s];
     const int lg = log2i(pl.n[s]);

@@ -11,8 +11,9 @@ struct MssArgs {
   long long L;
   int T, nwg;
   float alpha, eps, inv_cnt;
-  float* dpred;        // (B, L) or null
-  int accumulate;      // add into dpred instead of writing it (0 on the slab path)
+  const float* tmag;   // (B, T, n/2 + 1) target magnitudes |STFT_n(target)|, computed in float64
+                       // by mss_target_kernel (mss.hip) and rounded to float
+  float* dpred;        // (B, L) this size's gradient slab, or null
   float* edges;        // (B, n): gradient of the reflect-pad samples, head n/2 then tail n/2
   float* partial;      // (B, nwg, 2): per-workgroup sums of |dS| and |dlogS|
 };

@@ -431,8 +431,10 @@ class PerformanceNetFunction(torch.autograd.Function):
             for h in hooks:
                 h.ready(params)
         sink = module._grad_sink(on_ready if hooks else None)
-        module.__dict__["_mst_last_sink"] = sink  # tests inspect its join event
         g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need)
+        # the side stream's join event (None when the weight gradients ran on the compute
+        # stream): an Event, so no hook closure of this backward outlives it
+        module.__dict__["_mst_wgrad_joined"] = sink.joined
         for h in hooks:
             h.launch_remaining()
         ctx.state = None

@@ -147,9 +147,10 @@ def conv_like(*, B, M, Tn, srcs, Tv, taps, a, beta, g, A, A_off=0, sAm, sAc, sAt
     d.seed_dev = seed_dev.data_ptr() if seed_dev is not None else None
     d.splitk = splitk or _FORCE_SPLITK
     ref = ctypes.byref(d)
-    ws, nb = _workspace(lib.mst_conv_fwd_workspace_size(ref), A.device)
+    need = lib.mst_conv_fwd_workspace_size(ref)  # split-K: splits * M * N * 4 bytes
+    ws, nb = _workspace(need, A.device)
     _timed(lambda: L.check(lib.mst_conv_fwd_f32(ref, L.ptr(ws), nb, L.stream()), "mst_conv_fwd_f32"),
-           2.0 * M * B * Tn * d.Ctot * taps, "conv", (M, B * Tn, d.Ctot * taps, taps, a, nb))
+           2.0 * M * B * Tn * d.Ctot * taps, "conv", (M, B * Tn, d.Ctot * taps, taps, a, need))
 
 
 def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, ldc=0, ldt=0, scale=1.0, accumulate=False,
@@ -174,10 +175,11 @@ def wgrad_like(*, P, srcs, Tv, taps, a, beta, g, out, ldo, ldc=0, ldt=0, scale=1
     d.accumulate = 1 if accumulate else 0
     d.splitk = splitk or _FORCE_SPLITK
     ref = ctypes.byref(d)
-    ws, nb = _workspace(lib.mst_wgrad_workspace_size(ref), P.device)
+    need = lib.mst_wgrad_workspace_size(ref)  # split-K: splits * M * (source's C * taps) * 4 bytes
+    ws, nb = _workspace(need, P.device)
     _timed(lambda: L.check(lib.mst_conv_wgrad_f32(ref, L.ptr(ws), nb, L.stream()),
                            "mst_conv_wgrad_f32"), 2.0 * M * B * Tk * d.Ctot * taps, "wgrad",
-           (M, d.Ctot * taps, B * Tk, taps, a, nb))
+           (M, d.Ctot * taps, B * Tk, taps, a, need))
 
 
 def _wgrad_out(dW):

@@ -9,6 +9,7 @@ Python drop-ins use (include/mst.h); there is no CPU implementation (a CPU tenso
   stft_logpow / stft_power           preprocessing/preprocess.py:47-49
   stft_complex (frame-major)         librosa.stft behind model/inference.py:105-110
   istft (differentiable)             librosa.istft behind the same Griffin-Lim (+ istft_backward)
+  render_logpow (differentiable)     model/inference.py:109 (magnitude inversion) with a held phase
   melspectrogram                     tests/plot_spec.py:20
   griffinlim                         model/inference.py:105-110, tests/test_griffinlim.py:23
   mss_loss (differentiable)          README.md:23, model/train.py:119-123 (engel_loss stub)
@@ -136,6 +137,55 @@ def _istft_backward(ctx, g):
 
 
 istft.register_autograd(_istft_backward, setup_context=_istft_setup)
+
+
+@custom_op("mst::render_logpow", mutates_args=())
+def render_logpow(S: Tensor, P: Tensor) -> Tensor:
+    """(B, F, T) log-power, (B, T, F, 2) held complex spectrum -> (B, T, F, 2)
+    sqrt(expm1(clip(S, 0, 20))) * P / |P| (inference.py:109's inversion with P's phase)."""
+    S, P = _signal(S), _signal(P)
+    B, F, T = S.shape
+    if tuple(P.shape) != (B, T, F, 2):
+        raise ValueError("render_logpow: P must be (B, T, F, 2)")
+    X = torch.empty(B, T, F, 2, device=S.device, dtype=torch.float32)
+    L.check(L.load().mst_render_logpow_f32(L.ptr(S), L.ptr(P), B, F, T, L.ptr(X), L.stream()),
+            "render_logpow")
+    return X
+
+
+@render_logpow.register_fake
+def _render_fake(S, P):
+    B, F, T = S.shape
+    return S.new_empty(B, T, F, 2, dtype=torch.float32)
+
+
+@custom_op("mst::render_logpow_backward", mutates_args=())
+def render_logpow_backward(S: Tensor, P: Tensor, grad: Tensor) -> Tensor:
+    """d/dS of render_logpow with P held: Re(conj(P/|P|) grad) * e^S / (2 M) inside (0, 20)."""
+    S, P, g = _signal(S), _signal(P), _signal(grad)
+    B, F, T = S.shape
+    dS = torch.empty_like(S)
+    L.check(L.load().mst_render_logpow_bwd_f32(L.ptr(S), L.ptr(P), L.ptr(g), B, F, T, L.ptr(dS),
+                                               L.stream()), "render_logpow_backward")
+    return dS
+
+
+@render_logpow_backward.register_fake
+def _render_backward_fake(S, P, grad):
+    return torch.empty_like(S)
+
+
+def _render_setup(ctx, inputs, output):
+    S, P = inputs
+    ctx.save_for_backward(S, P)
+
+
+def _render_backward(ctx, g):
+    S, P = ctx.saved_tensors
+    return torch.ops.mst.render_logpow_backward(S, P, g), None
+
+
+render_logpow.register_autograd(_render_backward, setup_context=_render_setup)
 
 
 @custom_op("mst::melspectrogram", mutates_args=())
@@ -459,7 +509,8 @@ def _linear_backward(ctx, g):
 
 linear_ncl.register_autograd(_linear_backward, setup_context=_conv_setup)
 
-OPS = ("stft_logpow", "stft_power", "stft_complex", "istft", "istft_backward", "melspectrogram",
+OPS = ("stft_logpow", "stft_power", "stft_complex", "istft", "istft_backward", "render_logpow",
+       "render_logpow_backward", "melspectrogram",
        "griffinlim", "mss_loss", "l1_loss", "l1_loss_backward", "mse_loss", "onoff", "conv1d_k3",
        "conv1d_k3_backward", "conv_transpose1d", "conv_transpose1d_backward", "linear_ncl",
        "linear_ncl_backward")

@@ -100,43 +100,57 @@ def istft_autograd(X, hop=256):
     return y[0] if single else y
 
 
-class _LogpowToMag(torch.autograd.Function):
-    """M = sqrt(expm1(clip(S, 0, 20))) (inference.py:109); dM/dS = e^S / (2M) inside (0, 20)."""
-
-    @staticmethod
-    def forward(ctx, S):
-        M = torch.expm1(S.clamp(0, 20)).sqrt()
-        ctx.save_for_backward(S, M)
-        return M
-
-    @staticmethod
-    def backward(ctx, g):
-        S, M = ctx.saved_tensors
-        inside = (S > 0) & (S < 20)
-        d = torch.where(inside, torch.exp(S.clamp(0, 20)) / (2 * M.clamp_min(1e-30)),
-                        torch.zeros_like(S))
-        return g * d
+def render_logpow(S, P):
+    """(B, F, T) log-power -> (B, T, F, 2) complex spectrum sqrt(expm1(clip(S, 0, 20))) * P/|P|
+    (inference.py:109's inversion, with the phase of the held spectrum P: (B, T, F, 2) float or
+    (B, T, F) complex). One fused transpose kernel each way (render.hip); differentiable in S."""
+    if torch.is_complex(P):
+        P = torch.view_as_real(P)
+    return torch.ops.mst.render_logpow(S, P.detach().contiguous())
 
 
-def spectrogram_mss_loss(S_pred, target_audio, phase=None, hop=256, alpha=1.0, eps=1e-7,
-                         sizes=None):
-    """The README's intended loss (README.md:23) as a training loss on the
-    model's log-power output: render audio y = istft(sqrt(expm1(clip(S_pred,0,20))) * phase)
-    and take the multi-scale spectral loss against the target waveform. `phase` (B, T, F)
-    unit complex defaults to the target's own STFT phase (held constant); gradients flow to
-    S_pred through the iSTFT adjoint. S_pred: (B, 1025, T); target_audio: (B, hop*(T-1))."""
+MSS_PHASES = ("target", "griffinlim")
+
+
+def spectrogram_mss_loss(S_pred, target_audio=None, phase="target", hop=256, alpha=1.0, eps=1e-7,
+                         sizes=None, S_target=None, gl_iters=8):
+    """The README's intended loss (README.md:23; the reference's engel_loss stub,
+    train.py:119-123) as a training loss on the model's log-power output: render audio
+    y = istft(sqrt(expm1(clip(S_pred, 0, 20))) * phase) and take the multi-scale spectral loss
+    against the target waveform; gradients flow to S_pred through the iSTFT adjoint with the phase
+    held constant.
+
+    phase: "target"      the STFT phase of target_audio;
+           "griffinlim"  the phase of S_pred's own Griffin-Lim reconstruction (gl_iters iterations
+                         from all-ones phases, no gradient): the audio inference would synthesise
+                         (inference.py:105-110), rendered from the model's magnitude;
+           a tensor      any held (B, T, F, 2) / complex (B, T, F) spectrum.
+    target_audio: (B, hop (T - 1)) waveform, or None with S_target (B, F, T) log-power: the target
+    is then S_target's Griffin-Lim reconstruction (the reference's HDF5 data holds spectrograms
+    only, io_manager.py:64-76). Built-defined loss: parity unpinned against the reference."""
     B, F, T = S_pred.shape
-    if target_audio.shape != (B, hop * (T - 1)):
-        raise ValueError("target_audio must be (B, hop*(T-1))")
-    if phase is None:
-        with torch.no_grad():
-            Xt = stft_complex(target_audio.contiguous(), hop=hop, n_fft=2 * (F - 1))
-            phase = Xt / Xt.abs().clamp_min(1e-16)
-            phase = torch.where(Xt.abs() > 0, phase, torch.ones_like(phase))
-    M = _LogpowToMag.apply(S_pred)
-    X = M.transpose(1, 2) * phase
-    y = istft_autograd(X, hop)
-    return multiscale_spectral_loss(y, target_audio, alpha=alpha, eps=eps,
+    n_fft = 2 * (F - 1)
+    with torch.no_grad():
+        if target_audio is None:
+            if S_target is None:
+                raise ValueError("spectrogram_mss_loss needs target_audio or S_target")
+            target_audio = griffinlim(S_target, n_iter=gl_iters, hop_length=hop, init=None,
+                                      from_logpow=True)
+        if target_audio.shape != (B, hop * (T - 1)):
+            raise ValueError("target_audio must be (B, hop*(T-1))")
+        if isinstance(phase, torch.Tensor):
+            P = phase
+        elif phase == "target":
+            P = stft_complex(target_audio.contiguous(), hop=hop, n_fft=n_fft)
+        elif phase == "griffinlim":
+            y_gl = griffinlim(S_pred.detach(), n_iter=gl_iters, hop_length=hop, init=None,
+                              from_logpow=True)
+            P = stft_complex(y_gl, hop=hop, n_fft=n_fft)
+        else:
+            raise ValueError(f"phase={phase!r}: one of {MSS_PHASES} or a tensor")
+    X = render_logpow(S_pred, P)
+    y = torch.ops.mst.istft(X, int(hop))
+    return multiscale_spectral_loss(y, target_audio.detach(), alpha=alpha, eps=eps,
                                     sizes=MSS_SIZES if sizes is None else sizes)
 
 
@@ -267,4 +281,4 @@ def spectral_convergence(S, y, hop=256):
 __all__ = ["stft_logpow", "stft_power", "stft_complex", "istft", "melspectrogram", "mel_basis",
            "griffinlim", "random_angles", "spectral_convergence", "n_frames",
            "multiscale_spectral_loss", "MSS_SIZES", "math", "istft_autograd",
-           "spectrogram_mss_loss"]
+           "spectrogram_mss_loss", "render_logpow", "MSS_PHASES"]

@@ -255,6 +255,7 @@ class BackwardAdam:
         self.active = self.launched = False
         self.st = self.params = None
         self.updates = 0  # steps whose update ran inside backward
+        self.joined = None  # event of the last finish(): completes with that step's updates
         self.max_blocks = int(os.environ.get("MST_BWD_ADAM_BLOCKS", "256"))  # A/B tuning knob
 
     def _eligible(self):
@@ -348,15 +349,49 @@ def _cuda(t):
     return t if t.is_cuda else t.cuda(non_blocking=True)
 
 
-def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2):
-    """train.py:125-149 (same loop, loss and prints)."""
+LOSSES = ("l1", "mss", "l1+mss")
+
+
+def make_loss(name="l1", mss_phase="griffinlim", gl_iters=8, alpha=1.0, sizes=None, hop=256):
+    """The training loss, loss_fn(y_pred, target) on (B, 1025, T) log-power spectrograms:
+      l1      nn.L1Loss (train.py:132-135), the reference's loss;
+      mss     the README's multi-scale spectral loss (README.md:23; the engel_loss stub,
+              train.py:119-123) on rendered audio, spectral.spectrogram_mss_loss: the target is
+              the Griffin-Lim reconstruction of the target spectrogram (gl_iters iterations; the
+              HDF5 data holds no audio), the prediction is rendered with mss_phase's phase
+              ("griffinlim": its own reconstruction's, "target": the target reconstruction's);
+      l1+mss  their sum."""
+    if name not in LOSSES:
+        raise ValueError(f"loss {name!r}: one of {LOSSES}")
+    from . import spectral
+
+    def mss(y_pred, target):
+        if y_pred.shape != target.shape:
+            raise ValueError("the multi-scale loss needs T = 12 (mod 16) (model.py:229-232)")
+        with torch.no_grad():
+            y_t = spectral.griffinlim(target, n_iter=gl_iters, hop_length=hop, init=None,
+                                      from_logpow=True)
+        return spectral.spectrogram_mss_loss(y_pred, y_t, phase=mss_phase, hop=hop, alpha=alpha,
+                                             sizes=sizes, gl_iters=gl_iters)
+
+    if name == "l1":
+        return E.l1_loss
+    if name == "mss":
+        return mss
+    return lambda y_pred, target: E.l1_loss(y_pred, target) + mss(y_pred, target)
+
+
+def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2, loss_fn=None):
+    """train.py:125-149 (same loop, loss and prints); loss_fn defaults to train.py:132's L1
+    (make_loss selects the multi-scale spectral loss instead)."""
     model.train()
     train_loss = 0
+    loss_fn = loss_fn or E.l1_loss
     for batch_idx, (data, data_cond, target) in enumerate(train_loader):
         optimizer.zero_grad()
         split = torch.split(data, 128, dim=1)
         y_pred = model(_cuda(split[0]), _cuda(data_cond), _cuda(split[1]))
-        loss = E.l1_loss(y_pred, _cuda(target))
+        loss = loss_fn(y_pred, _cuda(target))
         loss.backward()
         dp.finish_gradients(model)  # no-op unless an overlapped DP all-reduce is attached
         iter_train_loss.append(loss.item())
@@ -453,6 +488,8 @@ def main(args, return_model=False):
     model.zero_grad()
     optimizer.zero_grad()
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, 'min')
+    loss_fn = make_loss(getattr(args, "loss", "l1"), mss_phase=getattr(args, "mss_phase", "griffinlim"),
+                        gl_iters=getattr(args, "gl_iters", 8))
     if args.data_dir and os.path.exists(args.data_dir + '_train.hdf5'):
         from .data import DeviceLoader, Process_Data
         train_loader, test_loader = Process_Data(args.data_dir, n_train_read=args.n_train_read,
@@ -478,7 +515,7 @@ def main(args, return_model=False):
     for epoch in range(hp.train_epoch):
         if hasattr(train_loader, "set_epoch"):
             train_loader.set_epoch(epoch)
-        loss = train(model, epoch, train_loader, optimizer, hp.iter_train_loss)
+        loss = train(model, epoch, train_loader, optimizer, hp.iter_train_loss, loss_fn=loss_fn)
         hp.loss_history.append(loss.item())
         if epoch % hp.test_freq == 0:
             test_loss = test(model, epoch, test_loader, scheduler, hp.iter_test_loss)
@@ -508,6 +545,12 @@ def parse_args(argv=None):
     parser.add_argument("--n-test-read", type=int, default=None)
     parser.add_argument("--batch-size", type=int, default=16)
     parser.add_argument("--frames", type=int, default=252)
+    parser.add_argument("-loss", type=str, default="l1", choices=LOSSES,
+                        help="l1 (train.py:132), the README's multi-scale spectral loss, or both")
+    parser.add_argument("-mss-phase", type=str, default="griffinlim", choices=("griffinlim", "target"),
+                        help="phase that renders the prediction for the multi-scale loss")
+    parser.add_argument("-gl-iters", type=int, default=8,
+                        help="Griffin-Lim iterations behind the multi-scale loss's audio")
     return parser.parse_args(argv)
 
 
@@ -515,4 +558,5 @@ if __name__ == "__main__":
     main(parse_args())
 
 
-__all__ = ["train", "test", "Adam", "make_optimizer", "hyperparams", "main", "np"]
+__all__ = ["train", "test", "Adam", "make_optimizer", "make_loss", "LOSSES", "hyperparams", "main",
+           "np"]

@@ -73,3 +73,9 @@ def model_inputs(B, T, seed=0, n_pitch=128, n_bins=1025):
     x_audio = uniform("x_audio", (B, n_bins, T), 0.0, 4.0, seed) ** 2 / 4.0
     target = uniform("target", (B, n_bins, T), 0.0, 4.0, seed) ** 2 / 4.0
     return x_midi, x_audio, cond.astype(np.float32), target
+
+
+def offgrid_target(B, T_out, seed=0, n_bins=1025):
+    """L1 target for an input length T whose output length T_out = 16 * floor(T / 16) + 12
+    differs from T (model.py:229-232): drawn at the output's length."""
+    return uniform("target_offgrid", (B, n_bins, T_out), 0.0, 4.0, seed) ** 2 / 4.0

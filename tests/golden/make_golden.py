@@ -12,6 +12,8 @@ entries and per-parameter gradient statistics.
 
 Usage:  python tests/golden/make_golden.py          (blocks, B=2/T=44, B=1/T=252)
         python tests/golden/make_golden.py bench    (B=32/T=252, the benchmarked config)
+        python tests/golden/make_golden.py t860     (B=2/T=860, the reference's own training
+                                                     chunk, and B=2/T=100, an off-grid length)
 """
 import os
 import sys
@@ -61,8 +63,18 @@ def grad_stats(module, prefix="g"):
     return out, names
 
 
+def out_len(T):
+    """PerformanceNet's output length (model.py:229-232: the up-kernels 6/4/3/2 give
+    16 * floor(T / 16) + 12), T itself only when T = 12 (mod 16)."""
+    return 16 * (T // 16) + 12
+
+
 def _run(net, B, T, dtype):
     xm, xa, cd, tg = (torch.from_numpy(a).to(dtype) for a in detinit.model_inputs(B, T))
+    if out_len(T) != T:
+        # off-grid length: the reference's L1Loss (train.py:132) needs a target of the output's
+        # length, so the target is drawn at that length (detinit.offgrid_target)
+        tg = torch.from_numpy(detinit.offgrid_target(B, out_len(T))).to(dtype)
     net.zero_grad(set_to_none=True)
     y = net(xm, xa, cd)
     loss = nn.L1Loss()(y, tg)
@@ -155,7 +167,7 @@ def full_model_lowmem(B, T, fname):
            "loss64": np.array(loss64, dtype=np.float64),
            "out_stat": np.array([yv.sum(), np.abs(yv).sum(), (yv * yv).sum()]),
            "out_idx": oidx, "out_val": yv[oidx].astype(np.float32), "out_val64": yv64[oidx],
-           "out_shape": np.array([B, 1025, T])}
+           "out_shape": np.array([B, 1025, out_len(T)])}
     names = list(g32)
     for n in names:
         g, g64 = g32[n], g64s[n]
@@ -272,6 +284,10 @@ def blocks():
 if __name__ == "__main__":
     if sys.argv[1:] == ["bench"]:  # the benchmarked configuration only (slow: ~minutes on CPU)
         full_model_lowmem(32, 252, "full_B32_T252.npz")
+        sys.exit(0)
+    if sys.argv[1:] == ["t860"]:  # the reference's training chunk (preprocess.py:42,66) + off-grid T
+        full_model_lowmem(2, 860, "full_B2_T860.npz")
+        full_model_lowmem(2, 100, "full_B2_T100.npz")
         sys.exit(0)
     blocks()
     full_model(2, 44, "full_B2_T44.npz")

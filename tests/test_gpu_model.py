@@ -304,10 +304,10 @@ def test_side_streams_joined_once_main_stream_synced(cuda):
             for _ in range(2):
                 opt.zero_grad()
                 E.l1_loss(net(xm, xa, cd), tg).backward()
-                sink = net.__dict__["_mst_last_sink"]
-                assert sink.side is not None and sink.joined is not None  # the side stream ran
+                joined = net.__dict__["_mst_wgrad_joined"]
+                assert joined is not None  # the side stream ran and was joined
                 torch.cuda.current_stream().synchronize()
-                assert sink.joined.query(), "a weight-gradient launch outlived the compute-stream sync"
+                assert joined.query(), "a weight-gradient launch outlived the compute-stream sync"
                 opt.step()
                 torch.cuda.current_stream().synchronize()
                 if overlap:
@@ -406,6 +406,116 @@ def test_full_model_bench_config_B32(cuda):
     print("B=32: split-K launches", len(split), "worst (ratio, ours, ref32) vs fp64:", worst[-4:])
     for ratio, ours, theirs, n in worst:
         assert ours <= max(4 * theirs, 1e-4), (n, ours, theirs)
+
+
+def _full_vs_fp64(net, g, y, loss):
+    """Loss, sampled outputs and sampled weight gradients vs a make_golden.py full_model_lowmem
+    fixture, with test_full_model_bench_config_B32's bounds. Returns the worst gradient rows."""
+    lv, lr = loss.item(), float(g["loss"])
+    assert abs(lv - lr) <= 1e-4 * abs(lr), (lv, lr)
+    assert tuple(y.shape) == tuple(g["out_shape"])
+    y64, y32 = g["out_val64"], g["out_val"].astype(np.float64)
+    yv = y.detach().double().cpu().numpy().ravel()[g["out_idx"]]
+    err = np.abs(yv - y64).max()
+    rel = np.linalg.norm(yv - y64) / np.linalg.norm(y64)
+    assert err <= 1e-4 * np.abs(y64).max(), (err, np.abs(y64).max())
+    assert rel <= 1e-4, rel
+    worst = []
+    for n, p in net.named_parameters():
+        if f"gnone:{n}" in g.files:
+            assert p.grad is None, n
+            continue
+        gv = p.grad.detach().double().cpu().numpy().ravel()[g[f"gidx:{n}"]]
+        g64, g32 = g[f"gval64:{n}"], g[f"gval:{n}"].astype(np.float64)
+        if _noise_bias(n):
+            wscale = np.abs(g[f"gval64:{n.replace('.bias', '.weight')}"]).max()
+            assert np.abs(gv).max() <= 1e-2 * wscale + 1e-9, n
+            continue
+        den = np.linalg.norm(g64) + 1e-30
+        ours, theirs = np.linalg.norm(gv - g64) / den, np.linalg.norm(g32 - g64) / den
+        worst.append((ours / max(theirs, 2.5e-5), ours, theirs, n))
+        assert ours <= max(4 * theirs, 1e-4), (n, ours, theirs)
+    worst.sort()
+    return err, rel, worst[-3:]
+
+
+@pytest.mark.parametrize("fname", ["full_B2_T860.npz", "full_B2_T100.npz"])
+def test_full_model_reference_lengths(cuda, fname):
+    """The reference's own training length and an off-grid one, vs the reference model
+    (make_golden.py t860: /root/reference/model/model.py in fp32 and fp64), bounds as in
+    test_full_model_bench_config_B32.
+    T = 860: 5 s @ 44.1 kHz = spc * wps frames (preprocess.py:24-25,40-42,66,86), the chunk the
+    reference trains on; its levels run at T = 860/430/215/107/53, so the deep layers take
+    split-K schedules and odd-length InstanceNorm rows the T = 44/252 fixtures never reach.
+    T = 100: 100 = 4 (mod 16), so the U-Net returns 16 * 6 + 12 = 108 frames (model.py:229-232),
+    the case the inference CLI meets on whole tracks; the L1 target is drawn at 108 frames."""
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd import kernels as K
+    g = np.load(os.path.join(GOLD, fname))
+    B, T = int(g["B"]), int(g["T"])
+    net = _det_model(cuda).eval()
+    xm, xa, cd, tg = _inputs(B, T, cuda)
+    Tout = int(g["out_shape"][2])
+    if Tout != T:
+        tg = torch.from_numpy(detinit.offgrid_target(B, Tout)).to(cuda)
+    log = []
+    K.gemm_timing(log)
+    try:
+        y = net(xm, xa, cd)
+        loss = E.l1_loss(y, tg)
+        loss.backward()
+    finally:
+        K.gemm_timing(None)
+    torch.cuda.synchronize()
+    err, rel, worst = _full_vs_fp64(net, g, y, loss)
+    split = sorted({(tag, *shp[:3], round(shp[-1] / (4.0 * shp[0] * shp[1]), 2))
+                    for _, _, _, tag, shp in log if shp and shp[-1] > 0})
+    print(f"B={B} T={T}: out {tuple(y.shape)}, max {err:.3e}, rel L2 {rel:.3e}; "
+          f"{len(log)} GEMM launches, split-K schedules (kind, M, N, K, splits): {split}; worst {worst}")
+
+
+def test_train_steps_reference_batch_B16_T860(cuda):
+    """The reference's default training shape: --batch-size 16 (train.py:219) on 860-frame
+    chunks (preprocess.py:42,66). Properties, since no CPU reference fits a GPU test's time at
+    this size: samples are independent (InstanceNorm is per sample, train.py:132's L1 is a mean),
+    so the B = 16 loss equals the mean of its two B = 8 halves' losses (1e-5 relative) and its
+    weight gradients the mean of theirs (rel L2 per parameter <= 1e-3: the halves run other
+    split-K schedules, i.e. other fp32 summation orders); then three Adam steps on the batch
+    stay finite and lower the loss."""
+    from ml_music_style_transfer_amd import engine as E
+    from ml_music_style_transfer_amd.train import make_optimizer
+    B, T = 16, 860
+    xm, xa, cd, tg = _inputs(B, T, cuda)
+    net = _det_model(cuda).eval()
+    grads, losses = [], []
+    for sl in (slice(0, B), slice(0, B // 2), slice(B // 2, B)):
+        net.zero_grad(set_to_none=True)
+        loss = E.l1_loss(net(xm[sl], xa[sl], cd[sl]), tg[sl])
+        loss.backward()
+        losses.append(loss.item())
+        grads.append({n: p.grad.detach().double().clone() for n, p in net.named_parameters()
+                      if p.grad is not None})
+    assert abs(losses[0] - 0.5 * (losses[1] + losses[2])) <= 1e-5 * abs(losses[0]), losses
+    worst = 0.0
+    for n, g0 in grads[0].items():
+        if _noise_bias(n):
+            continue
+        gh = 0.5 * (grads[1][n] + grads[2][n])
+        r = ((g0 - gh).norm() / (gh.norm() + 1e-30)).item()
+        worst = max(worst, r)
+        assert r <= 1e-3, (n, r)
+    opt = make_optimizer(net, lr=1e-3)
+    hist = []
+    for _ in range(3):
+        opt.zero_grad()
+        loss = E.l1_loss(net(xm, xa, cd), tg)
+        loss.backward()
+        opt.step()
+        hist.append(loss.item())
+    assert all(np.isfinite(hist)) and hist[-1] < hist[0], hist
+    assert all(torch.isfinite(p).all() for p in net.parameters())
+    print(f"B=16 T=860: loss {losses[0]:.6f} = mean of halves {losses[1]:.6f}, {losses[2]:.6f}; "
+          f"worst grad rel L2 vs halves {worst:.2e}; Adam losses {hist}")
 
 
 def _grads_once(cuda):

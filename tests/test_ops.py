@@ -26,6 +26,9 @@ def test_fake_shapes():
         X = torch.ops.mst.stft_complex(x, 2048, 256, 0)
         assert X.shape == (3, 65, 1025, 2)
         assert torch.ops.mst.istft(X, 256).shape == (3, 16384)
+        Sl = torch.empty(3, 1025, 65, device="cuda")
+        assert torch.ops.mst.render_logpow(Sl, X).shape == X.shape
+        assert torch.ops.mst.render_logpow_backward(Sl, X, X).shape == Sl.shape
         st = torch.empty(128, dtype=torch.int32, device="cuda")
         w = torch.empty(2000, device="cuda")
         assert torch.ops.mst.melspectrogram(x, 2048, 256, 0, st, st, st, w).shape == (3, 128, 65)
@@ -94,6 +97,7 @@ def test_opcheck_spectral(cuda):
     torch.library.opcheck(torch.ops.mst.istft, (X, 256))
     S = torch.ops.mst.stft_logpow(x, 2048, 256, 0)
     torch.library.opcheck(torch.ops.mst.griffinlim, (S, 2, 256, 0.99, None, True))
+    torch.library.opcheck(torch.ops.mst.render_logpow, (S.clone().requires_grad_(True), X.detach()))
     p = x.clone().requires_grad_(True)
     t = _r(2, 8192, seed=2).float().to(cuda)
     torch.library.opcheck(torch.ops.mst.mss_loss, (p, t, [2048, 256, 64], 1.0, 1e-7, True))
