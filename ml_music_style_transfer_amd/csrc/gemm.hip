@@ -205,6 +205,11 @@ struct GP {
   // stream-K (sk_L > 0): the grid's G workgroups each run sk_L consecutive iterations of the
   // flattened (tile, 32-deep K tile) space of sk_I = tiles * nk iterations
   long long sk_L, sk_I;
+  // pre-split operand planes (gemm_p_kernel): 3 bf16 planes each, [rows][pld] (k contiguous)
+  const __bf16* pA;
+  const __bf16* pB;
+  long long psa, psb;  // plane strides (elements)
+  int pld;             // row stride = padded K (a multiple of BK)
 };
 
 // Tile-order index -> (M tile, N tile): runs of GM M-tiles x all N-tiles, M fastest within a
@@ -882,6 +887,196 @@ static int wg_vec() {
   return v;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pre-split operand planes (round 5). The register-split kernels above split every loaded fp32
+// element into its three bf16 pieces once per tile pass, i.e. once for every output tile that
+// reads it (5.5 VALU per element, three LDS stores per 8 elements: VALU:MFMA 4.5-5.7 in PMC).
+// Here a pack kernel splits each operand element ONCE per GEMM into three bf16 planes in HBM,
+// laid out as the GEMM reads them ([rows][K], K contiguous, zero padding and every range mask
+// baked in), and gemm_p_kernel moves 16-byte pieces of the planes straight into LDS with
+// buffer_load ... lds (no VGPRs, no VALU): its main loop is ds_read + MFMA. LDS image, fragment
+// reads and MFMA order are the 128 x 256 kernel's (pl_off swizzle: the per-lane source address
+// takes the inverse permutation, the destination stays lane-linear).
+//
+// Weight gradients (K = (b, t), t padded to Tp): A planes = P (dY or X) rows m, B planes = rows
+// n = c * taps + tap of X(b, c, a t + beta + g tap) over both concat sources, masked.
+struct PackArgs {
+  __bf16* out;   // 3 planes of rows x ld bf16, plane stride ps
+  long long ps;
+  int ld, rows, taps;
+  int B, Tk, Tp;
+  int a, beta, g, Tv;
+  const float* x0;
+  long long sb0;
+  int sc0, C0, T0, off0;
+  const float* x1;
+  long long sb1;
+  int sc1, T1, off1;
+};
+
+// one thread per 8 consecutive k of one row: 8 source values -> three 16-byte plane stores
+__global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
+  const int q8 = a.ld >> 3;
+  const long long total = (long long)a.rows * q8;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / q8), kq = (int)(i - (long long)row * q8);
+    const int c = row / a.taps, tap = row - c * a.taps;
+    const bool s1 = c >= a.C0;
+    const float* x = s1 ? a.x1 : a.x0;
+    const long long sb = s1 ? a.sb1 : a.sb0;
+    const int cs = s1 ? c - a.C0 : c, sc = s1 ? a.sc1 : a.sc0;
+    const int Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
+    const int k0 = 8 * kq, b = k0 / a.Tp, t0 = k0 - b * a.Tp;
+    const float* xr = x + (long long)b * sb + (long long)cs * sc;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int t = t0 + e;
+      const int tin = a.a * t + a.beta + a.g * tap;
+      const bool ok = b < a.B && t < a.Tk && (unsigned)tin < (unsigned)a.Tv &&
+                      (unsigned)(tin + off) < (unsigned)Ts;
+      v[e] = ok ? xr[tin + off] : 0.f;
+    }
+    bf16x8 hi, mid, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const Bf3 t3 = split1(v[e]);
+      hi[e] = t3.h;
+      mid[e] = t3.m;
+      lo[e] = t3.l;
+    }
+    __bf16* o = a.out + (long long)row * a.ld + k0;
+    *reinterpret_cast<bf16x8*>(o) = hi;
+    *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
+    *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
+  }
+}
+
+constexpr int STAGE_P = STAGE_BF;  // 72 KB of bf16 per stage: A 3 x [128][32], B 3 x [256][32]
+
+template <bool WG>
+__device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int n_t, int kt0,
+                                            int kt1, int split, int tid) {
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m0 = m_t * BM, n0 = n_t * BNW;
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.pA, (short)0,
+                                                      (int)(3 * p.psa * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.pB, (short)0,
+                                                      (int)(3 * p.psb * 2), 0x00020000);
+  // this wave's 9 of the stage's 72 one-KB pieces: j = wave + 8 i; j < 24 are A (plane j / 8,
+  // rows 16 (j % 8) ..), the rest B (plane (j - 24) / 16, rows 16 ((j - 24) % 16) ..). Lane l
+  // fills bytes 16 l of its piece: tile row r0 + l / 4, LDS slot l % 4 = quad q ^ pl_swz(row).
+  uint32_t voff[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = wave + 8 * i;
+    const bool a = j < 24;
+    const int jj = a ? j : j - 24;
+    const int plane = a ? jj >> 3 : jj >> 4;
+    const int r = (a ? jj & 7 : jj & 15) * 16 + (lane >> 2);
+    const int q = (lane & 3) ^ pl_swz(r);
+    const int row = (a ? m0 : n0) + r;
+    const bool in = row < (a ? p.M : p.N);
+    const long long e = plane * (a ? p.psa : p.psb) + (long long)row * p.pld + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : OOB;
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    const int soff = kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int j = wave + 8 * i;  // wave-uniform: A or B by a scalar branch
+      auto* dst = (__attribute__((address_space(3))) void*)(lds + (stage * STAGE_P) * 2 + j * 1024);
+      if (j < 24) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+    }
+  };
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (kt0 < kt1) {
+    issue(0, kt0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int st = (kt - kt0) & 1;
+      if (kt + 1 < kt1) issue(st ^ 1, kt + 1);
+      const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE_P;
+      const __bf16* Bp = Ap + 3 * PLANE;
+      const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+#pragma unroll
+      for (int s2 = 0; s2 < BK / 16; ++s2) {
+        const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, 2 * s2 + h);
+        const Split3 b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 * s2 + h);
+        const Split3 a0 = ld_planes<PLANE>(Ap, ra0, 2 * s2 + h);
+        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+        const Split3 a1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 * s2 + h);
+        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+      }
+      // the next stage's DMA has landed and every wave is done reading this one
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // epilogue: accumulators -> LDS tile (128 x 256 floats, aliasing the stages) -> rows
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl = 128 * g + wn * 64 + j * 32 + r32;
+        Cs[ml * BNW + nl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int nl = tid & (BNW - 1);
+  const int n = n0 + nl;
+  if (n < p.N) {
+    for (int ml = tid >> 8; ml < BM; ml += NTHRW / BNW) {
+      const int m = m0 + ml;
+      if (m >= p.M) break;
+      const float v = Cs[ml * BNW + nl];
+      if (p.splitk > 1) p.ws[((long long)split * p.M + m) * p.N + n] = v;
+      else if constexpr (WG) wgrad_store(p, m, n, v);
+      else conv_store(p, m, n, v);
+    }
+  }
+}
+
+template <bool WG>
+__global__ __launch_bounds__(NTHRW, 1) void gemm_p_kernel(const GP p) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_W_FLOATS * 4];
+  const int nx = (p.N + BNW - 1) / BNW, ny = (p.M + BM - 1) / BM;
+  const int W = nx * ny * (int)gridDim.z;
+  const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
+  const int split = t / (nx * ny);
+  int m_t, n_t;
+  tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
+  const int kt0 = (int)((long long)split * p.nk / p.splitk);
+  const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
+  tile_pass_p<WG>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
+}
+
+static int wg_planes() {  // weight gradients on pre-split planes; MST_WG_PLANES=0: register split
+  static const int v = [] {
+    const char* e = getenv("MST_WG_PLANES");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
 // Schedules. Data-parallel / split-K: one (tile, split) per workgroup, grid (nx, ny, splitk).
 // Stream-K: a 1-D grid of G workgroups (one full residency wave); workgroup v runs iterations
 // [v L, v L + L) of the flattened (tile, K tile) space, i.e. the tail of one tile, whole tiles,
@@ -1333,6 +1528,143 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
   return MST_OK;
 }
 
+// Weight gradient on pre-split planes: ONE GEMM over both concat sources (columns n = c taps + tap
+// of the concatenated channels, which is where the per-source launches' outputs sit too).
+// Workspace: [split-K slabs][A planes][B planes], 256-byte aligned pieces.
+struct PlanesWG {
+  GP p;
+  PackArgs pa, pb;
+  size_t slab_bytes, a_bytes, b_bytes;
+};
+
+static size_t round256(size_t x) { return (x + 255) / 256 * 256; }
+
+int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
+  MST_REQUIRE(d && d->P && d->src[0].p && d->out);
+  MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tk > 0 && d->Ctot > 0 && d->src[0].C > 0 && taps_ok(d->taps));
+  MST_REQUIRE(d->g >= 0 && d->a >= 1);
+  MST_REQUIRE(d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
+  MST_REQUIRE(d->src[1].C <= 0 || d->src[1].p);
+  GP& p = w.p;
+  p = GP{};
+  p.M = d->M;
+  p.N = d->Ctot * d->taps;
+  MST_REQUIRE(p.N < (1 << 22));
+  const int Tp = d->Tk <= 16 ? 16 : ceil_div(d->Tk, BK) * BK;
+  const int Bp = Tp == 16 ? (d->B + 1) / 2 * 2 : d->B;  // K a multiple of BK
+  const long long Kp = (long long)Bp * Tp;
+  MST_REQUIRE(Kp < (1 << 30));
+  p.pld = (int)Kp;
+  p.K = (int)Kp;
+  p.nk = (int)(Kp / BK);
+  p.psa = (long long)p.M * Kp;
+  p.psb = (long long)p.N * Kp;
+  // the plane descriptors address 3 planes with 32-bit byte offsets
+  MST_REQUIRE(6 * p.psa < (long long)OOB && 6 * p.psb < (long long)OOB);
+  p.out = d->out;
+  p.ldo = d->ldo;
+  p.taps = d->taps;
+  if (d->ldc == 0 && d->ldt == 0) {
+    p.ldc = d->taps;
+    p.ldt = 1;
+  } else {
+    p.ldc = d->ldc;
+    p.ldt = d->ldt;
+  }
+  p.ocustom = !(p.ldc == d->taps && p.ldt == 1);
+  p.inv_taps = 1.0f / (float)d->taps;
+  p.scale = d->scale;
+  p.accumulate = d->accumulate;
+  p.splitk = choose_splitk(p.M, p.N, p.nk, d->splitk > 0 ? d->splitk : 0, 1, BNW);
+  PackArgs& a = w.pa;
+  a = PackArgs{};
+  a.ps = p.psa;
+  a.ld = (int)Kp;
+  a.rows = p.M;
+  a.taps = 1;
+  a.B = d->B;
+  a.Tk = d->Tk;
+  a.Tp = Tp;
+  a.a = 1;
+  a.Tv = d->Tk;
+  a.x0 = d->P;
+  a.sb0 = d->sPb;
+  a.sc0 = d->sPc;
+  a.C0 = p.M;
+  a.T0 = d->Tk;
+  PackArgs& b = w.pb;
+  b = a;
+  b.ps = p.psb;
+  b.rows = p.N;
+  b.taps = d->taps;
+  b.a = d->a;
+  b.beta = d->beta;
+  b.g = d->g;
+  b.Tv = d->Tv;
+  b.x0 = d->src[0].p;
+  b.sb0 = d->src[0].sb;
+  b.sc0 = d->src[0].sc;
+  b.C0 = d->src[1].C > 0 ? d->src[0].C : d->Ctot;
+  b.T0 = d->src[0].T;
+  b.off0 = d->src[0].off;
+  if (d->src[1].C > 0) {
+    b.x1 = d->src[1].p;
+    b.sb1 = d->src[1].sb;
+    b.sc1 = d->src[1].sc;
+    b.T1 = d->src[1].T;
+    b.off1 = d->src[1].off;
+  }
+  w.slab_bytes = p.splitk > 1 ? round256((size_t)p.splitk * p.M * p.N * sizeof(float)) : 0;
+  w.a_bytes = round256((size_t)(3 * p.psa) * 2);
+  w.b_bytes = round256((size_t)(3 * p.psb) * 2);
+  return MST_OK;
+}
+
+int launch_pack(const PackArgs& a, hipStream_t st) {
+  const long long total = (long long)a.rows * (a.ld >> 3);
+  long long blocks = (total + 255) / 256;
+  if (blocks > 32768) blocks = 32768;
+  hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  MST_CHECK_LAUNCH();
+  return MST_OK;
+}
+
+int run_wgrad_planes(PlanesWG& w, float* ws, hipStream_t st) {
+  GP& p = w.p;
+  char* base = reinterpret_cast<char*>(ws);
+  p.ws = ws;
+  w.pa.out = reinterpret_cast<__bf16*>(base + w.slab_bytes);
+  w.pb.out = reinterpret_cast<__bf16*>(base + w.slab_bytes + w.a_bytes);
+  p.pA = w.pa.out;
+  p.pB = w.pb.out;
+  int rc = launch_pack(w.pa, st);
+  if (rc) return rc;
+  rc = launch_pack(w.pb, st);
+  if (rc) return rc;
+  dim3 grid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk);
+  hipLaunchKernelGGL((gemm_p_kernel<true>), grid, dim3(NTHRW), 0, st, p);
+  MST_CHECK_LAUNCH();
+  if (p.splitk > 1) {
+    const long long total = (long long)p.M * p.N;
+    if (total % 4 == 0 && total < (1ll << 31)) {
+      int blocks = (int)((total / 4 + 255) / 256);
+      if (blocks > 8192) blocks = 8192;
+      hipLaunchKernelGGL((splitk_reduce4_kernel<true>), dim3(blocks), dim3(256), 0, st, p);
+    } else {
+      int blocks = (int)((total + 255) / 256);
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL((splitk_reduce_kernel<true>), dim3(blocks), dim3(256), 0, st, p);
+    }
+    MST_CHECK_LAUNCH();
+  }
+  return MST_OK;
+}
+
+// the planes path serves auto and split-K schedules (stream-K requests take the register path)
+bool use_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
+  return d && d->splitk >= 0 && wg_planes() && build_wgrad_planes(d, w) == MST_OK;
+}
+
 int wgrad_sources(const mst_wgrad_desc* d, mst_src* srcs, float** outs) {
   MST_REQUIRE(d && d->src[0].C + (d->src[1].C > 0 ? d->src[1].C : 0) == d->Ctot);
   srcs[0] = d->src[0];
@@ -1368,6 +1700,8 @@ size_t mst_wgrad_workspace_size(const mst_wgrad_desc* d) {
   mst_src srcs[2];
   float* outs[2];
   if (!d) return 0;
+  PlanesWG w;
+  if (use_wgrad_planes(d, w)) return w.slab_bytes + w.a_bytes + w.b_bytes;
   const int ns = wgrad_sources(d, srcs, outs);
   if (ns < 1) return 0;
   size_t need = 0;
@@ -1384,6 +1718,12 @@ int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* ws, size_t ws_bytes, void
   mst_src srcs[2];
   float* outs[2];
   if (!d) return MST_EINVAL;
+  {
+    PlanesWG w;
+    if (use_wgrad_planes(d, w) && ws && ws_bytes >= w.slab_bytes + w.a_bytes + w.b_bytes &&
+        ((uintptr_t)ws & 255) == 0)
+      return run_wgrad_planes(w, ws, (hipStream_t)stream);
+  }
   const int ns = wgrad_sources(d, srcs, outs);
   if (ns < 1) return MST_EINVAL;
   GP ps[2];

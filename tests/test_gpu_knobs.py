@@ -21,7 +21,8 @@ KNOBS = [
     {"MST_GEMM_WIDE": "0"},         # conv / dgrad on the 128 x 128 kernel
     {"MST_GEMM_SCHED": "sk"},       # stream-K for every GEMM
     {"MST_SPLITK_TAU": "1e-9"},     # split-K cost model pushed to no split
-    {"MST_WG_VEC": "0"},            # wgrad: dword loads in the unmasked K classes too
+    {"MST_WG_PLANES": "0"},         # wgrad on the register-split 128 x 128 kernel (K classes)
+    {"MST_WG_PLANES": "0", "MST_WG_VEC": "0"},  # ... with dword loads in the unmasked classes too
     {"MST_IN_SEG": "0"},            # one InstanceNorm row per wave
     {"MST_ADAM_VARIANT": "1p"},     # Adam: one float4 group per thread, plain loads/stores
     {"MST_GL_FRAMES": "8", "MST_GL_CHUNK_MB": "1"},  # Griffin-Lim: 8-frame workgroups, 1-clip chunks

@@ -479,9 +479,11 @@ def test_train_steps_reference_batch_B16_T860(cuda):
     chunks (preprocess.py:42,66). Properties, since no CPU reference fits a GPU test's time at
     this size: samples are independent (InstanceNorm is per sample, train.py:132's L1 is a mean),
     so the B = 16 loss equals the mean of its two B = 8 halves' losses (1e-5 relative) and its
-    weight gradients the mean of theirs (rel L2 per parameter <= 1e-3: the halves run other
-    split-K schedules, i.e. other fp32 summation orders); then three Adam steps on the batch
-    stay finite and lower the loss."""
+    weight gradients the mean of theirs. The halves run other split-K schedules, i.e. other fp32
+    summation orders, and this network's fp32 gradients are ill-conditioned (L1 sign, ReLU /
+    LeakyReLU kinks, maxpool ties flip under rounding), so each parameter's rel L2 gap is held to
+    4x the reference's own fp32-vs-fp64 gap for that parameter at T = 860 (full_B2_T860.npz),
+    floor 1e-3. Then three Adam steps on the batch stay finite and lower the loss."""
     from ml_music_style_transfer_amd import engine as E
     from ml_music_style_transfer_amd.train import make_optimizer
     B, T = 16, 860
@@ -496,14 +498,17 @@ def test_train_steps_reference_batch_B16_T860(cuda):
         grads.append({n: p.grad.detach().double().clone() for n, p in net.named_parameters()
                       if p.grad is not None})
     assert abs(losses[0] - 0.5 * (losses[1] + losses[2])) <= 1e-5 * abs(losses[0]), losses
-    worst = 0.0
+    fx = np.load(os.path.join(GOLD, "full_B2_T860.npz"))
+    worst = []
     for n, g0 in grads[0].items():
         if _noise_bias(n):
             continue
         gh = 0.5 * (grads[1][n] + grads[2][n])
         r = ((g0 - gh).norm() / (gh.norm() + 1e-30)).item()
-        worst = max(worst, r)
-        assert r <= 1e-3, (n, r)
+        gap = float(fx[f"gstat:{n}"][3] / max(fx[f"gstat:{n}"][4], 1e-30))  # ref fp32 vs fp64
+        worst.append((r / max(gap, 2.5e-4), r, gap, n))
+        assert r <= max(4 * gap, 1e-3), (n, r, gap)
+    worst = sorted(worst)[-3:]
     opt = make_optimizer(net, lr=1e-3)
     hist = []
     for _ in range(3):
@@ -515,7 +520,7 @@ def test_train_steps_reference_batch_B16_T860(cuda):
     assert all(np.isfinite(hist)) and hist[-1] < hist[0], hist
     assert all(torch.isfinite(p).all() for p in net.parameters())
     print(f"B=16 T=860: loss {losses[0]:.6f} = mean of halves {losses[1]:.6f}, {losses[2]:.6f}; "
-          f"worst grad rel L2 vs halves {worst:.2e}; Adam losses {hist}")
+          f"worst (ratio to ref fp32 gap, rel L2 vs halves, gap, name) {worst}; Adam losses {hist}")
 
 
 def _grads_once(cuda):

@@ -5,9 +5,10 @@ kernel, iSTFT with its adjoint, mss kernels, the model's backward) against a tor
 restatement of the same pipeline on the CPU (oracle/model_ref.py's functional PerformanceNet,
 torch.istft, torch.stft), with the phase held as the loss holds it.
 
-Tolerances: loss 1e-4 relative (north_star); the gradient at the model output within 2 % rel L2
-of float64 (the MSS's 1/(S + eps) factor, test_istft_grad.py) and every sampled weight gradient
-within max(4 x the torch fp32 CPU gap, 2 %) rel L2 of float64. The loss is this build's
+Tolerances: loss 1e-4 relative (north_star); the gradient at the model output (the render /
+iSTFT / loss chain evaluated in float64 at this model output) within max(2 x torch fp32's gap,
+2 %) rel L2 (the MSS's 1/(S + eps) factor, test_istft_grad.py), and every sampled weight gradient
+within max(4 x the torch fp32 CPU gap, 2 %) rel L2 of the float64 step. The loss is this build's
 definition (the reference has only the stub): parity unpinned against the reference.
 """
 import numpy as np
@@ -38,12 +39,16 @@ def _torch_mss(y, yt, sizes):
     return tot
 
 
-def _cpu_step(dtype, P, yt, B, T, sizes):
-    """The restated step in `dtype` on the CPU: forward, render with P's phase, istft, MSS, grads."""
-    p = {k: v.to(dtype).requires_grad_(True) for k, v in R.det_params().items()}
-    xm, xa, cd, _ = (torch.from_numpy(a).to(dtype) for a in detinit.model_inputs(B, T))
-    S = R.forward(p, xm, xa, cd)
-    S.retain_grad()
+def _cpu_step(dtype, P, yt, B, T, sizes, S_in=None):
+    """The restated step in `dtype` on the CPU: forward, render with P's phase, istft, MSS, grads.
+    With S_in the chain starts at that model output (no forward; parameter grads None)."""
+    p = {k: v.to(dtype).requires_grad_(True) for k, v in R.det_params().items()} if S_in is None else {}
+    if S_in is None:
+        xm, xa, cd, _ = (torch.from_numpy(a).to(dtype) for a in detinit.model_inputs(B, T))
+        S = R.forward(p, xm, xa, cd)
+        S.retain_grad()
+    else:
+        S = S_in.to(dtype).clone().requires_grad_(True)
     U = P / P.abs().clamp_min(1e-300)
     U = torch.where(P.abs() > 0, U, torch.ones_like(U)).to(torch.complex128 if dtype == torch.float64
                                                             else torch.complex64)
@@ -79,12 +84,19 @@ def test_performancenet_step_with_mss_loss(cuda, phase):
         src = yt if phase == "target" else spectral.griffinlim(S.detach(), n_iter=4, init=None,
                                                                from_logpow=True)
         P = spectral.stft_complex(src).cpu().to(torch.complex128)  # (B, T, F)
-    l64, dS64, g64 = _cpu_step(torch.float64, P, yt.cpu().double(), B, T, sizes)
-    l32, dS32, g32 = _cpu_step(torch.float32, P, yt.cpu(), B, T, sizes)
+    l64, _, g64 = _cpu_step(torch.float64, P, yt.cpu().double(), B, T, sizes)
+    l32, _, g32 = _cpu_step(torch.float32, P, yt.cpu(), B, T, sizes)
     assert abs(loss.item() - l64) <= 1e-4 * abs(l64), (loss.item(), l64, l32)
+    # the render / iSTFT / loss chain alone, in float64 at OUR model output: dM/dS = e^S / (2 M)
+    # grows without bound as S -> 0+, so the chain is compared at the same S, not through two
+    # forwards that round differently around S = 0
+    Sg = S.detach().double().cpu()
+    _, dS64, _ = _cpu_step(torch.float64, P, yt.cpu().double(), B, T, sizes, S_in=Sg)
+    _, dS32, _ = _cpu_step(torch.float32, P, yt.cpu(), B, T, sizes, S_in=Sg)
     dS = S.grad.double().cpu()
     rel_out = ((dS - dS64).norm() / dS64.norm()).item()
-    assert rel_out <= 2e-2, rel_out
+    gap_out = ((dS32.double() - dS64).norm() / dS64.norm()).item()
+    assert rel_out <= max(2 * gap_out, 2e-2), (rel_out, gap_out)
     worst = []
     for n, q in net.named_parameters():
         if q.grad is None or g64.get(n) is None:
@@ -95,8 +107,8 @@ def test_performancenet_step_with_mss_loss(cuda, phase):
         r32 = g32[n].double().reshape(-1)[idx]
         den = r64.norm().item() + 1e-30
         e_ours, e_ref = (ours - r64).norm().item() / den, (r32 - r64).norm().item() / den
-        if r64.abs().max().item() < 1e-12:  # IN-preceded conv biases: exact gradient 0
-            continue
+        if n.endswith(".bias") and not (n.startswith("dense_concats") or n == "lastconv.bias"):
+            continue  # conv biases followed by InstanceNorm: exact gradient 0 (rounding noise only)
         worst.append((e_ours, e_ref, n))
         assert e_ours <= max(4 * e_ref, 2e-2), (n, e_ours, e_ref)
     opt = make_optimizer(net, lr=1e-3)
@@ -104,7 +116,7 @@ def test_performancenet_step_with_mss_loss(cuda, phase):
     assert all(torch.isfinite(q).all() for q in net.parameters())
     worst.sort()
     print(f"phase={phase}: loss {loss.item():.6f} vs fp64 {l64:.6f} (fp32 CPU {l32:.6f}); "
-          f"dL/dS rel L2 {rel_out:.2e}; worst weight-gradient gaps (ours, torch fp32, name) {worst[-3:]}")
+          f"dL/dS rel L2 {rel_out:.2e} (torch fp32 {gap_out:.2e}); worst weight-gradient gaps (ours, torch fp32, name) {worst[-3:]}")
 
 
 def test_train_loop_with_mss_loss(cuda):

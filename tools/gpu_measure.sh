@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 for what in "$@"; do
   case $what in
     tests)
-      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 120 --timeout-method thread \
         > "$OUT/pytest_gpu.log" 2>&1 ;;
     bench)
       timeout -k 10 400 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
@@ -77,6 +77,13 @@ for what in "$@"; do
       timeout -k 10 300 python -u tools/mss_probe.py > "$OUT/mss_probe.txt" 2>&1 ;;
     benchnoaux)
       timeout -k 10 300 python -u bench.py --no-aux > "$OUT/bench_noaux.json" 2> "$OUT/bench_noaux.err" ;;
+    planes)
+      make -C tools/micro gemm_planes > "$OUT/planes_build.log" 2>&1
+      timeout -k 10 120 tools/micro/gemm_planes check > "$OUT/gemm_planes.txt" 2>&1 ;;
+    rest)
+      timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_mss_train.py tests/test_gpu_spectral.py \
+        tests/test_istft_grad.py tests/test_ops.py -m gpu -x -v -rP --timeout 120 --timeout-method thread \
+        -k "B16 or mss or spectral or istft or opcheck or multiscale or stft or mel or griffin" > "$OUT/pytest_rest.log" 2>&1 ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     *) echo "unknown step $what"; exit 2 ;;

@@ -1,0 +1,398 @@
+// Microbenchmark (dev tool): a bf16x6 NT GEMM on PRE-SPLIT operand planes, C[m][n] = sum_k
+// A[m][k] B[n][k] with A = A0 + A1 + A2 and B = B0 + B1 + B2 held as three bf16 planes each in HBM
+// ([rows][K], K contiguous). The tiles go straight into LDS by buffer_load ... lds (no VGPRs, no
+// split VALU), in the 128 x 256 kernel's swizzled plane layout (gemm.hip), so the main loop is
+// ds_read + MFMA only. Question it answers: what TF/s (fp32 products) a pre-split operand path
+// reaches on the training step's GEMM shapes, against the register-split kernels' 130-165.
+//
+// build: make -C tools/micro gemm_planes ; run: tools/micro/gemm_planes
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+constexpr int BM = 128, BN = 256, BK = 32, NT = 512;
+constexpr int PA = BM * BK, PB = BN * BK;           // bf16 elements per A / B plane tile
+constexpr int STAGE = 3 * PA + 3 * PB;              // 72 KB of bf16 per stage
+constexpr int LDS_BYTES = 2 * STAGE * 2;            // two stages: 144 KB
+
+__device__ __forceinline__ int pl_swz(int row) {
+  return ((row >> 2) & 1) | (((row >> 1) ^ (row >> 3)) & 1) << 1;
+}
+__device__ __forceinline__ int pl_off(int row, int q) { return row * BK + 8 * (q ^ pl_swz(row)); }
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+template <int PS>
+__device__ __forceinline__ Split3 ld_planes(const __bf16* base, int row, int q) {
+  const __bf16* p = base + pl_off(row, q);
+  Split3 s;
+  s.h = *reinterpret_cast<const bf16x8*>(p);
+  s.m = *reinterpret_cast<const bf16x8*>(p + PS);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * PS);
+  return s;
+}
+__device__ __forceinline__ f32x16 mfma_x6(const Split3& a, const Split3& b, f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, acc, 0, 0, 0);
+  return acc;
+}
+
+struct PP {
+  const __bf16* A;  // 3 planes, plane stride sa elements, row stride lda
+  const __bf16* B;
+  long long sa, sb;
+  int M, N, K, lda, ldb;
+  float* C;
+  int ldc;
+};
+
+__device__ __forceinline__ int xcd_order(int w, int W) {
+  const int q = W >> 3, r = W & 7, xcd = w & 7;
+  return xcd * q + min(xcd, r) + (w >> 3);
+}
+
+__global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(const PP p) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  const int t = xcd_order(blockIdx.x + nx * blockIdx.y, nx * ny);
+  // runs of 8 M tiles x all N tiles (gemm.hip tile_of)
+  const int GM = ny < 8 ? ny : 8, grp = t / (GM * nx), fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM, tg = t - grp * GM * nx;
+  const int m0 = (fm + tg % gm) * BM, n0 = (tg / gm) * BN;
+  // operand descriptors: rows past M / N read zeros (bounded buffer loads)
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0,
+                                                      (int)((2 * p.sa + (long long)p.M * p.lda) * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0,
+                                                      (int)((2 * p.sb + (long long)p.N * p.ldb) * 2), 0x00020000);
+  // this wave's 9 glds instructions per stage: j = wave + 8 i; j < 24 are A (plane j / 8, rows
+  // 16 (j % 8) ..), the rest B (plane (j - 24) / 16, rows 16 ((j - 24) % 16) ..). Lane l fills
+  // LDS bytes 16 l of the instruction's 1 KB: row r0 + l / 4, slot l % 4 = quad q ^ swz(row).
+  uint32_t voff[9];
+  int isA[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = wave + 8 * i;
+    const bool a = j < 24;
+    const int jj = a ? j : j - 24;
+    const int plane = a ? jj / 8 : jj / 16;
+    const int r = (a ? jj % 8 : jj % 16) * 16 + (lane >> 2);
+    const int q = (lane & 3) ^ pl_swz(r);
+    const long long row = a ? (long long)(m0 + r) : (long long)(n0 + r);
+    const bool in = a ? (m0 + r < p.M) : (n0 + r < p.N);
+    const long long e = plane * (a ? p.sa : p.sb) + row * (a ? p.lda : p.ldb) + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
+    isA[i] = a;
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    const int soff = kt * BK * 2;  // k offset in bytes
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int j = wave + 8 * i;
+      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE * 2 + j * 1024);
+      if (isA[i]) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+    }
+  };
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (p.K + BK - 1) / BK;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    if (kt + 1 < nk) issue(st ^ 1, kt + 1);
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE;
+    const __bf16* Bp = Ap + 3 * PA;
+    const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const Split3 b0 = ld_planes<PB>(Bp, rb0, 2 * s + h), b1 = ld_planes<PB>(Bp, rb0 + 32, 2 * s + h);
+      const Split3 a0 = ld_planes<PA>(Ap, ra0, 2 * s + h);
+      acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+      acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+      const Split3 a1 = ld_planes<PA>(Ap, ra0 + 32, 2 * s + h);
+      acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+      acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  // epilogue through LDS (128 x 256 floats aliases the stages)
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl = 128 * g + wn * 64 + j * 32 + r32;
+        Cs[ml * BN + nl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int nl = tid & (BN - 1);
+  if (n0 + nl < p.N)
+    for (int ml = tid >> 8; ml < BM && m0 + ml < p.M; ml += 2) p.C[(long long)(m0 + ml) * p.ldc + n0 + nl] = Cs[ml * BN + nl];
+}
+
+// ---- variant 2: 256 x 256 tile, BK = 16, three LDS stages (48 KB each) with one stage of
+// buffer_load ... lds in flight across each barrier (counted vmcnt, raw s_barrier). 8 waves as
+// 2 (M) x 4 (N), wave tile 128 x 64 (4 x 2 blocks of 32 x 32). Plane rows are 32 B (two 16-byte
+// quads), quad slot XOR (row >> 3) & 1: conflict-free for the ds_read_b128 fragment reads.
+constexpr int B2M = 256, B2N = 256, B2K = 16;
+constexpr int P2 = 256 * B2K;          // bf16 elements per plane tile
+constexpr int STAGE2 = 6 * P2;         // A 3 planes + B 3 planes = 48 KB
+constexpr int NST2 = 3;
+
+__device__ __forceinline__ int off2(int row, int q) { return row * B2K + 8 * (q ^ ((row >> 3) & 1)); }
+__device__ __forceinline__ Split3 ld2(const __bf16* base, int row, int q) {
+  const __bf16* p = base + off2(row, q);
+  Split3 s;
+  s.h = *reinterpret_cast<const bf16x8*>(p);
+  s.m = *reinterpret_cast<const bf16x8*>(p + P2);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * P2);
+  return s;
+}
+
+__global__ __launch_bounds__(NT, 1) void gemm_planes2_kernel(const PP p) {
+  __shared__ __attribute__((aligned(16))) char lds[NST2 * STAGE2 * 2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = (p.N + B2N - 1) / B2N, ny = (p.M + B2M - 1) / B2M;
+  const int t = xcd_order(blockIdx.x + nx * blockIdx.y, nx * ny);
+  const int GM = ny < 8 ? ny : 8, grp = t / (GM * nx), fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM, tg = t - grp * GM * nx;
+  const int m0 = (fm + tg % gm) * B2M, n0 = (tg / gm) * B2N;
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0,
+                                                      (int)((2 * p.sa + (long long)p.M * p.lda) * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0,
+                                                      (int)((2 * p.sb + (long long)p.N * p.ldb) * 2), 0x00020000);
+  // 48 one-KB pieces per stage, 6 per wave: j = wave + 8 i; j < 24 A (plane j / 8, rows
+  // 32 (j % 8) ..), else B. Lane l: row r0 + l / 2, slot l % 2 = quad q ^ swz(row).
+  uint32_t voff[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int j = wave + 8 * i;
+    const bool a = j < 24;
+    const int jj = a ? j : j - 24;
+    const int plane = jj >> 3;
+    const int r = (jj & 7) * 32 + (lane >> 1);
+    const int q = (lane & 1) ^ ((r >> 3) & 1);
+    const long long row = a ? (long long)(m0 + r) : (long long)(n0 + r);
+    const bool in = a ? (m0 + r < p.M) : (n0 + r < p.N);
+    const long long e = plane * (a ? p.sa : p.sb) + row * (a ? p.lda : p.ldb) + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    const int soff = kt * B2K * 2;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int j = wave + 8 * i;
+      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE2 * 2 + j * 1024);
+      if (j < 24) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+    }
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  const int r32 = lane & 31, h = lane >> 5;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (p.K + B2K - 1) / B2K;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) issue(st == 0 ? 2 : st - 1, kt + 2);  // the stage read one iteration ago
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE2;
+    const __bf16* Bp = Ap + 3 * P2;
+    const Split3 b0 = ld2(Bp, wn * 64 + r32, h), b1 = ld2(Bp, wn * 64 + 32 + r32, h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const Split3 a = ld2(Ap, wm * 128 + 32 * i + r32, h);
+      acc[i][0] = mfma_x6(a, b0, acc[i][0]);
+      acc[i][1] = mfma_x6(a, b1, acc[i][1]);
+    }
+    // retire the next stage's DMA (this wave's part), keep the one after it in flight
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    st = st == 2 ? 0 : st + 1;
+  }
+  // epilogue straight from the accumulators (lane: column r32, rows in the registers)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + 32 * j + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 128 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < p.M && n < p.N) p.C[(long long)m * p.ldc + n] = acc[i][j][r];
+      }
+    }
+}
+
+// reference: C = sum_k (A0+A1+A2)(B0+B1+B2) in double (naive)
+__global__ void ref_kernel(const PP p, double* Cr) {
+  const int m = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= p.N) return;
+  double s = 0;
+  for (int k = 0; k < p.K; ++k) {
+    double a = 0, b = 0;
+    for (int pl = 0; pl < 3; ++pl) {
+      a += (double)(float)p.A[pl * p.sa + (long long)m * p.lda + k];
+      b += (double)(float)p.B[pl * p.sb + (long long)n * p.ldb + k];
+    }
+    s += a * b;
+  }
+  Cr[(long long)m * p.N + n] = s;
+}
+
+static unsigned short f2bf(float x) {  // round to nearest even
+  unsigned u;
+  std::memcpy(&u, &x, 4);
+  u += 0x7FFF + ((u >> 16) & 1);
+  return (unsigned short)(u >> 16);
+}
+static float bf2f(unsigned short b) {
+  unsigned u = (unsigned)b << 16;
+  float x;
+  std::memcpy(&x, &u, 4);
+  return x;
+}
+static void split3(float x, unsigned short* o) {
+  o[0] = f2bf(x);
+  const float r1 = x - bf2f(o[0]);
+  o[1] = f2bf(r1);
+  o[2] = f2bf(r1 - bf2f(o[1]));
+}
+
+int main(int argc, char** argv) {
+  struct Shape {
+    int M, N, K;
+    const char* what;
+  } shapes[] = {
+      {2048, 2048, 2048, "square 2048"},
+      {4096, 4096, 4096, "square 4096"},
+      {1536, 13824, 8064, "wgrad audio L0 conv2 (M=Cout, N=3Cin, K=B T)"},
+      {2048, 9216, 4032, "wgrad audio L1"},
+      {3072, 18432, 2016, "wgrad audio L2"},
+      {1024, 6144, 8064, "wgrad up3 conv1"},
+      {2048, 8064, 4608, "conv fwd L1 audio (M=Cout, N=B T, K=3 Cin)"},
+      {1536, 8064, 4608, "conv fwd L0 audio"},
+  };
+  const bool check = argc > 1;
+  for (const Shape& s : shapes) {
+    const int Kp = (s.K + 31) / 32 * 32;
+    PP p{};
+    p.M = s.M, p.N = s.N, p.K = Kp, p.lda = Kp, p.ldb = Kp, p.ldc = s.N;
+    p.sa = (long long)s.M * Kp, p.sb = (long long)s.N * Kp;
+    std::vector<unsigned short> ha(3 * p.sa), hb(3 * p.sb);
+    srand(1);
+    for (long long i = 0; i < (long long)s.M * Kp; ++i) {
+      unsigned short o[3];
+      split3((float)((double)rand() / RAND_MAX * 2.0 - 1.0), o);
+      for (int pl = 0; pl < 3; ++pl) ha[pl * p.sa + i] = o[pl];
+    }
+    for (long long i = 0; i < (long long)s.N * Kp; ++i) {
+      unsigned short o[3];
+      split3((float)((double)rand() / RAND_MAX * 2.0 - 1.0), o);
+      for (int pl = 0; pl < 3; ++pl) hb[pl * p.sb + i] = o[pl];
+    }
+    __bf16 *da, *db;
+    float* dc;
+    CK(hipMalloc(&da, ha.size() * 2));
+    CK(hipMalloc(&db, hb.size() * 2));
+    CK(hipMalloc(&dc, (size_t)s.M * s.N * 4));
+    CK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
+    p.A = da, p.B = db, p.C = dc;
+   for (int var = 1; var <= 2; ++var) {
+    dim3 grid = var == 1 ? dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM)
+                         : dim3((s.N + B2N - 1) / B2N, (s.M + B2M - 1) / B2M);
+    auto launch = [&]() {
+      if (var == 1) hipLaunchKernelGGL(gemm_planes_kernel, grid, dim3(NT), 0, 0, p);
+      else hipLaunchKernelGGL(gemm_planes2_kernel, grid, dim3(NT), 0, 0, p);
+    };
+    CK(hipMemset(dc, 0, (size_t)s.M * s.N * 4));
+    launch();
+    CK(hipDeviceSynchronize());
+    if (check) {
+      double* dr;
+      CK(hipMalloc(&dr, (size_t)s.M * s.N * 8));
+      hipLaunchKernelGGL(ref_kernel, dim3((s.N + 255) / 256, s.M), dim3(256), 0, 0, p, dr);
+      CK(hipDeviceSynchronize());
+      std::vector<double> r((size_t)s.M * s.N);
+      std::vector<float> c((size_t)s.M * s.N);
+      CK(hipMemcpy(r.data(), dr, r.size() * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost));
+      double worst = 0, scale = 0;
+      for (size_t i = 0; i < r.size(); ++i) {
+        worst = fmax(worst, fabs(c[i] - r[i]));
+        scale = fmax(scale, fabs(r[i]));
+      }
+      printf("check v%d %-45s max|err| %.3e of max|C| %.3e (%.2e)\n", var, s.what, worst, scale, worst / scale);
+      CK(hipFree(dr));
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int reps = 20;
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < reps; ++i) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    const double tf = 2.0 * s.M * s.N * s.K / (ms * 1e-3) / 1e12;
+    printf("v%d %-50s M %5d N %5d K %5d tiles %4d  %.3f ms  %.1f TF/s fp32-equiv (%.3f of 416.7)\n", var,
+           s.what, s.M, s.N, s.K, grid.x * grid.y, ms, tf, tf / 416.7);
+   }
+    CK(hipFree(da));
+    CK(hipFree(db));
+    CK(hipFree(dc));
+  }
+  return 0;
+}
