@@ -228,6 +228,9 @@ def main():
     ap.add_argument("--adam-overlap", action="store_true",
                     help="Adam per bucket inside backward on a side stream (train.BackwardAdam) "
                          "instead of one launch in opt.step()")
+    ap.add_argument("--loss", default="l1", choices=["l1", "mss", "l1+mss"],
+                    help="training loss: train.py:132's L1 (the headline), the README's multi-scale "
+                         "spectral loss on audio rendered with the target's phase, or both")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,7 +285,7 @@ def main():
     comm_on = [True]  # off only for the exposed-communication leg after the timed region
     gstep = None
     if args.graph:
-        if world > 1 or args.adam_overlap:
+        if world > 1 or args.adam_overlap or args.loss != "l1":
             raise SystemExit("--graph: single GPU, no --adam-overlap")
         from ml_music_style_transfer_amd.graphs import GraphedTrainStep
         gstep = GraphedTrainStep(model, opt, warmup=1)
@@ -291,7 +294,16 @@ def main():
     adam_ev = []       # HIP events around opt.step() in the timed steps (the adam_kernel leg)
     adam_on = [False]
 
-    def step():
+    def loss_of(y, target, which):
+        if which == "l1":
+            return E.l1_loss(y, target)
+        # the README's loss (README.md:23) on audio rendered from the prediction with the target
+        # clip's STFT phase; the target waveform is the clip itself
+        mss = spectral.spectrogram_mss_loss(y, tgt_audio, phase="target", hop=HOP)
+        return mss if which == "mss" else E.l1_loss(y, target) + mss
+
+    def step(which=None):
+        which = which or args.loss
         if gstep is not None and graph_on[0]:
             target = spectral.stft_logpow(tgt_audio, hop=HOP)
             x_audio = spectral.stft_logpow(ref_audio, hop=HOP)
@@ -302,7 +314,7 @@ def main():
         x_audio = spectral.stft_logpow(ref_audio, hop=HOP)          # style reference spec
         split = torch.split(data, 128, dim=1)                      # train.py:130
         y = model(split[0], x_audio, split[1])
-        loss = E.l1_loss(y, target)
+        loss = loss_of(y, target, which)
         loss.backward()               # overlapped bucket all-reduces start inside backward
         if world > 1 and args.no_overlap and comm_on[0]:
             dp.allreduce_gradients(model)
@@ -397,8 +409,11 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (16 kHz piano clips per SURVEY 8(d); random-init PerformanceNet weights)",
-        "config": {"workload": "PerformanceNet train step: STFT front end + fwd + L1 + bwd"
+        "config": {"workload": "PerformanceNet train step: STFT front end + fwd + "
+                               + {"l1": "L1", "mss": "multi-scale spectral loss (rendered audio)",
+                                  "l1+mss": "L1 + multi-scale spectral loss"}[args.loss] + " + bwd"
                                + (" + RCCL all-reduce" if world > 1 else "") + " + Adam",
+                   "loss": args.loss,
                    "global_batch": world * B, "batch_per_gpu": B, "seq_len": T_FRAMES,
                    "sample_rate": SR, "n_fft": 2048, "hop": HOP, "parallelism": f"dp{world}"},
         "roofline": {
@@ -451,6 +466,11 @@ def main():
         out["config"]["hipgraph"] = True
     if not args.no_aux:
         out["aux"] = aux_legs(world, rank, dev, cpu=not args.no_cpu_baseline)
+        if args.loss == "l1" and gstep is None:
+            try:  # the same step with the README's loss (after the timed region)
+                out["aux"]["train_step_mss"] = mss_step_leg(step, world, dev, B, args)
+            except Exception as e:  # a report leg must not cost the measured line
+                out["aux"]["train_step_mss"] = {"error": repr(e)[:200]}
         try:  # reference inference call (inference.py:74-91): B = 1, one 4 s chunk
             from ml_music_style_transfer_amd.graphs import inference_step_times
             out["aux"]["inference_b1"] = {k: (round(v, 4) if isinstance(v, float) else v)
@@ -464,6 +484,29 @@ def main():
         torch.distributed.destroy_process_group()
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def mss_step_leg(step, world, dev, B, args, reps=5):
+    """The benchmarked step with the multi-scale spectral loss as the training loss (L1 + MSS on
+    audio rendered with the target's phase: train.make_loss's 'l1+mss' with the bench's own target
+    clips), timed like the headline (barrier + synchronize brackets, max over ranks)."""
+    for _ in range(2):
+        step("l1+mss")
+    torch.cuda.synchronize()
+    if world > 1:
+        dt = _timed_max(lambda: step("l1+mss"), reps, dev)
+    else:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            step("l1+mss")
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    ms = 1000.0 * dt / reps
+    return {"metric": "training-step spectrogram-frames/sec with L1 + multi-scale spectral loss",
+            "value": round(world * B * T_FRAMES / (dt / reps), 1), "unit": "spectrogram-frames/s",
+            "ms_per_step": round(ms, 3), "steps": reps, "loss": "l1+mss",
+            "workload": "the headline step, loss = L1 + spectral.spectrogram_mss_loss(phase='target') "
+                        "(render kernel, iSTFT + adjoint, 6-size loss kernels)"}
 
 
 def _timed_max(fn, reps, dev):

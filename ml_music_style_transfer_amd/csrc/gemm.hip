@@ -914,42 +914,51 @@ struct PackArgs {
   int sc1, T1, off1;
 };
 
-// one thread per 8 consecutive k of one row: 8 source values -> three 16-byte plane stores
+// One thread per (channel, 8 consecutive k), grid-stride over channels x ld/8 items (short rows,
+// T = 15 .. 63, pack several channels per workgroup), writing them for every tap (rows
+// c taps + tap) from one read of the source. Loads are raw buffer loads through one descriptor
+// per source; an element outside its ranges (t >= Tk, b >= B, input time outside [0, Tv) or the
+// source) gets the OOB offset: hardware zero, no branches.
 __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
   const int q8 = a.ld >> 3;
-  const long long total = (long long)a.rows * q8;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int row = (int)(i / q8), kq = (int)(i - (long long)row * q8);
-    const int c = row / a.taps, tap = row - c * a.taps;
+  const int chans = a.rows / a.taps;
+  const rsrc_t r0 = mk_rsrc(a.x0, (long long)(a.B - 1) * a.sb0 + (long long)(a.C0 - 1) * a.sc0 + a.T0);
+  const rsrc_t r1 = a.x1 ? mk_rsrc(a.x1, (long long)(a.B - 1) * a.sb1 +
+                                             (long long)(chans - a.C0 - 1) * a.sc1 + a.T1)
+                         : r0;
+  const long long total = (long long)chans * q8;
+  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total;
+       it += (long long)gridDim.x * 256) {
+    const int c = (int)(it / q8), kq = (int)(it - (long long)c * q8);
     const bool s1 = c >= a.C0;
-    const float* x = s1 ? a.x1 : a.x0;
-    const long long sb = s1 ? a.sb1 : a.sb0;
-    const int cs = s1 ? c - a.C0 : c, sc = s1 ? a.sc1 : a.sc0;
+    const int cs = s1 ? c - a.C0 : c;
     const int Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
     const int k0 = 8 * kq, b = k0 / a.Tp, t0 = k0 - b * a.Tp;
-    const float* xr = x + (long long)b * sb + (long long)cs * sc;
-    float v[8];
+    const int base = b * (int)(s1 ? a.sb1 : a.sb0) + cs * (s1 ? a.sc1 : a.sc0) + off;
+    for (int tap = 0; tap < a.taps; ++tap) {
+      float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int t = t0 + e;
-      const int tin = a.a * t + a.beta + a.g * tap;
-      const bool ok = b < a.B && t < a.Tk && (unsigned)tin < (unsigned)a.Tv &&
-                      (unsigned)(tin + off) < (unsigned)Ts;
-      v[e] = ok ? xr[tin + off] : 0.f;
-    }
-    bf16x8 hi, mid, lo;
+      for (int e = 0; e < 8; ++e) {
+        const int t = t0 + e;
+        const int tin = a.a * t + a.beta + a.g * tap;
+        const bool ok = b < a.B && t < a.Tk && (unsigned)tin < (unsigned)a.Tv &&
+                        (unsigned)(tin + off) < (unsigned)Ts;
+        const uint32_t vo = ok ? (uint32_t)(base + tin) * 4u : OOB;
+        v[e] = s1 ? ldb(r1, vo) : ldb(r0, vo);
+      }
+      bf16x8 hi, mid, lo;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const Bf3 t3 = split1(v[e]);
-      hi[e] = t3.h;
-      mid[e] = t3.m;
-      lo[e] = t3.l;
+      for (int e = 0; e < 8; ++e) {
+        const Bf3 t3 = split1(v[e]);
+        hi[e] = t3.h;
+        mid[e] = t3.m;
+        lo[e] = t3.l;
+      }
+      __bf16* o = a.out + (long long)(c * a.taps + tap) * a.ld + k0;
+      *reinterpret_cast<bf16x8*>(o) = hi;
+      *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
+      *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
     }
-    __bf16* o = a.out + (long long)row * a.ld + k0;
-    *reinterpret_cast<bf16x8*>(o) = hi;
-    *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
-    *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
   }
 }
 
@@ -1212,11 +1221,15 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
 // Split-K from a wave-quantisation cost model. 256 CUs x occ resident workgroups = the slots;
 // a workgroup's time is ~ (its K tiles) x tau. At occ = 2 a trailing partial wave of <= 256
 // workgroups runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave;
-// at occ = 1 (the 128 x 256 kernel) a lone workgroup runs no faster than in a full wave, so a
-// partial wave costs a whole one (MST_W_PARTIAL). Split-K adds a slab round trip (s + 2 passes
-// over M x N floats) plus a launch.
+// at occ = 1 (the 128 x 256 kernels) a lone workgroup runs no faster than in a full wave, so a
+// partial wave "should" cost a whole one, but charging it 1.0 (more splits) ran the training step
+// 0.8-1.6 % SLOWER (36.65-36.82 vs 37.10-37.24 ms, two same-box alternations,
+// profiles/r05/ab_step_w_partial.jsonl; the serialised GEMM leg itself ran faster, 159 -> 167
+// TF/s for conv/dgrad): beside the side-stream weight gradients the extra slab traffic and reduce
+// launches cost more than the quantisation they remove. MST_W_PARTIAL keeps 0.55, the measured
+// winner. Split-K adds a slab round trip (s + 2 passes over M x N floats) plus a launch.
 #ifndef MST_W_PARTIAL
-#define MST_W_PARTIAL 1.0
+#define MST_W_PARTIAL 0.55
 #endif
 int choose_splitk(int M, int N, int nk, int req, int occ, int bn = BN) {
   if (req > 0) return req < nk ? req : (nk > 0 ? nk : 1);
@@ -1614,6 +1627,11 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
     b.T1 = d->src[1].T;
     b.off1 = d->src[1].off;
   }
+  for (const PackArgs* q : {&a, &b}) {  // 32-bit byte offsets through each source's descriptor
+    const int C1 = q->rows / q->taps - q->C0;
+    MST_REQUIRE((long long)(q->B - 1) * q->sb0 + (long long)(q->C0 - 1) * q->sc0 + q->T0 < (1ll << 29));
+    MST_REQUIRE(!q->x1 || (long long)(q->B - 1) * q->sb1 + (long long)(C1 - 1) * q->sc1 + q->T1 < (1ll << 29));
+  }
   w.slab_bytes = p.splitk > 1 ? round256((size_t)p.splitk * p.M * p.N * sizeof(float)) : 0;
   w.a_bytes = round256((size_t)(3 * p.psa) * 2);
   w.b_bytes = round256((size_t)(3 * p.psb) * 2);
@@ -1621,9 +1639,9 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
 }
 
 int launch_pack(const PackArgs& a, hipStream_t st) {
-  const long long total = (long long)a.rows * (a.ld >> 3);
-  long long blocks = (total + 255) / 256;
-  if (blocks > 32768) blocks = 32768;
+  const long long items = (long long)(a.rows / a.taps) * (a.ld >> 3);
+  long long blocks = (items + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   MST_CHECK_LAUNCH();
   return MST_OK;

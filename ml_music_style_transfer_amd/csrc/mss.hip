@@ -528,15 +528,25 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
   for (int rd = 0; rd < MSS_TROUNDS; ++rd) {
     const int t0 = blk * PER_WG + (rd * MSS_TW + wave) * FBT;  // this wave's first frame
     if (t0 >= T) break;                                        // wave-uniform
-    // load + window: z_j = w_2j x_2j + i w_2j+1 x_2j+1 (periodic Hann in float64, reflect pad)
-#pragma unroll 4
-    for (int e = lane; e < FBT * HALF; e += 64) {
-      const int u = e / HALF, j = e - u * HALF;
+    // load + window: z_j = w_2j x_2j + i w_2j+1 x_2j+1 (periodic Hann in float64, reflect pad).
+    // All of the batch's samples are loaded before any is used (KT per lane in flight): loads
+    // under the per-element LDS stores were waited for one element at a time (590 us per call).
+    constexpr int KT = FBT * HALF / 64;  // samples pairs per lane: 8 (n <= 1024) or 16 (n = 2048)
+    float xa[KT], xb[KT];
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      const int e = lane + 64 * kk, u = e / HALF, j = e - u * HALF;
       const int t = min(t0 + u, T - 1);
       const int s0 = t * H + 2 * j - HALF;
+      xa[kk] = x[reflect(s0, L)];
+      xb[kk] = x[reflect(s0 + 1, L)];
+    }
+#pragma unroll
+    for (int kk = 0; kk < KT; ++kk) {
+      const int e = lane + 64 * kk, u = e / HALF, j = e - u * HALF;
       const d2 c0 = twd(qt, 2 * j, N), c1 = twd(qt, 2 * j + 1, N);  // W_N^k: cos(2 pi k / N)
       const double w0 = 0.5 - 0.5 * c0.x, w1 = 0.5 - 0.5 * c1.x;
-      S[e] = dk(w0 * (double)x[reflect(s0, L)], w1 * (double)x[reflect(s0 + 1, L)]);
+      S[e] = dk(w0 * (double)xa[kk], w1 * (double)xb[kk]);
     }
     wave_sync();
     wave_fft_d<LOG2N - 1, BWT>(S, qt, lane);

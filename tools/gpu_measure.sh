@@ -22,6 +22,19 @@ for what in "$@"; do
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmc_fetch.log" 2>&1
       timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmc_write.log" 2>&1 ;;
+    pmcgemm)
+      timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
+        --output-format csv -d "$OUT/pmcgemm/p1" -o run -- \
+        python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmcgemm.log" 2>&1 ;;
+    pmcall)  # FETCH / WRITE passes over the bench step and over each aux leg (traffic JSONs)
+      for w in step frontend griffinlim mss; do
+        if [ $w = step ]; then cmd="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0";
+        else cmd="bench_aux.py --workload $w --no-cpu-baseline --no-parity --steps 2 --warmup 1"; fi
+        for c in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d "$OUT/pmc_${w}_$c" -o run -- \
+            python3 $cmd > "$OUT/pmc_${w}_$c.log" 2>&1
+        done
+      done ;;
     pmcaux)
       timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmcaux_fetch" -o run -- \
         python3 bench_aux.py --workload frontend --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmcaux_fetch.log" 2>&1

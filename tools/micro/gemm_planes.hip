@@ -273,6 +273,102 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes2_kernel(const PP p) {
     }
 }
 
+// ---- variant 3: 128 x 128 tile, BK = 16, three 24 KB stages, 256 threads (2 x 2 waves of 64 x 64),
+// TWO workgroups per CU: one workgroup's barrier bubble is filled by the other's MFMAs.
+constexpr int P3 = 128 * B2K;   // bf16 elements per plane tile
+constexpr int STAGE3 = 6 * P3;  // 24 KB
+__device__ __forceinline__ Split3 ld3(const __bf16* base, int row, int q) {
+  const __bf16* p = base + off2(row, q);
+  Split3 s;
+  s.h = *reinterpret_cast<const bf16x8*>(p);
+  s.m = *reinterpret_cast<const bf16x8*>(p + P3);
+  s.l = *reinterpret_cast<const bf16x8*>(p + 2 * P3);
+  return s;
+}
+
+__global__ __launch_bounds__(256, 2) void gemm_planes3_kernel(const PP p) {
+  __shared__ __attribute__((aligned(16))) char lds[3 * STAGE3 * 2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = (p.N + 127) / 128, ny = (p.M + 127) / 128;
+  const int t = xcd_order(blockIdx.x + nx * blockIdx.y, nx * ny);
+  const int GM = ny < 8 ? ny : 8, grp = t / (GM * nx), fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM, tg = t - grp * GM * nx;
+  const int m0 = (fm + tg % gm) * 128, n0 = (tg / gm) * 128;
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0,
+                                                      (int)((2 * p.sa + (long long)p.M * p.lda) * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0,
+                                                      (int)((2 * p.sb + (long long)p.N * p.ldb) * 2), 0x00020000);
+  // 24 one-KB pieces per stage, 6 per wave: j = wave + 4 i; j < 12 A (plane j / 4, rows 32 (j % 4)), else B
+  uint32_t voff[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int j = wave + 4 * i;
+    const bool a = j < 12;
+    const int jj = a ? j : j - 12;
+    const int plane = jj >> 2;
+    const int r = (jj & 3) * 32 + (lane >> 1);
+    const int q = (lane & 1) ^ ((r >> 3) & 1);
+    const long long row = a ? (long long)(m0 + r) : (long long)(n0 + r);
+    const bool in = a ? (m0 + r < p.M) : (n0 + r < p.N);
+    const long long e = plane * (a ? p.sa : p.sb) + row * (a ? p.lda : p.ldb) + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    const int soff = kt * B2K * 2;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int j = wave + 4 * i;
+      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE3 * 2 + j * 1024);
+      if (j < 12) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+    }
+  };
+  const int wm = wave >> 1, wn = wave & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (p.K + B2K - 1) / B2K;
+  issue(0, 0);
+  if (nk > 1) issue(1, 1);
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 2 < nk) issue(st == 0 ? 2 : st - 1, kt + 2);
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE3;
+    const __bf16* Bp = Ap + 3 * P3;
+    const Split3 b0 = ld3(Bp, wn * 64 + r32, h), b1 = ld3(Bp, wn * 64 + 32 + r32, h);
+    const Split3 a0 = ld3(Ap, wm * 64 + r32, h);
+    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+    const Split3 a1 = ld3(Ap, wm * 64 + 32 + r32, h);
+    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+    if (kt + 2 < nk) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    st = st == 2 ? 0 : st + 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + 32 * j + r32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < p.M && n < p.N) p.C[(long long)m * p.ldc + n] = acc[i][j][r];
+      }
+    }
+}
+
 // reference: C = sum_k (A0+A1+A2)(B0+B1+B2) in double (naive)
 __global__ void ref_kernel(const PP p, double* Cr) {
   const int m = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -348,12 +444,14 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
     p.A = da, p.B = db, p.C = dc;
-   for (int var = 1; var <= 2; ++var) {
+   for (int var = 1; var <= 3; ++var) {
     dim3 grid = var == 1 ? dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM)
-                         : dim3((s.N + B2N - 1) / B2N, (s.M + B2M - 1) / B2M);
+              : var == 2 ? dim3((s.N + B2N - 1) / B2N, (s.M + B2M - 1) / B2M)
+                         : dim3((s.N + 127) / 128, (s.M + 127) / 128);
     auto launch = [&]() {
       if (var == 1) hipLaunchKernelGGL(gemm_planes_kernel, grid, dim3(NT), 0, 0, p);
-      else hipLaunchKernelGGL(gemm_planes2_kernel, grid, dim3(NT), 0, 0, p);
+      else if (var == 2) hipLaunchKernelGGL(gemm_planes2_kernel, grid, dim3(NT), 0, 0, p);
+      else hipLaunchKernelGGL(gemm_planes3_kernel, grid, dim3(256), 0, 0, p);
     };
     CK(hipMemset(dc, 0, (size_t)s.M * s.N * 4));
     launch();
