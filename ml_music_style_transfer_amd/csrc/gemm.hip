@@ -926,10 +926,10 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
   const rsrc_t r1 = a.x1 ? mk_rsrc(a.x1, (long long)(a.B - 1) * a.sb1 +
                                              (long long)(chans - a.C0 - 1) * a.sc1 + a.T1)
                          : r0;
-  const long long total = (long long)chans * q8;
-  for (long long it = (long long)blockIdx.x * 256 + threadIdx.x; it < total;
-       it += (long long)gridDim.x * 256) {
-    const int c = (int)(it / q8), kq = (int)(it - (long long)c * q8);
+  const int total = chans * q8;  // < 2^31: checked by the host (32-bit index math: a 64-bit
+                                 // division per item made the pack 30 % slower)
+  for (int it = blockIdx.x * 256 + threadIdx.x; it < total; it += gridDim.x * 256) {
+    const int c = it / q8, kq = it - c * q8;
     const bool s1 = c >= a.C0;
     const int cs = s1 ? c - a.C0 : c;
     const int Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
@@ -937,14 +937,30 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
     const int base = b * (int)(s1 ? a.sb1 : a.sb0) + cs * (s1 ? a.sc1 : a.sc0) + off;
     for (int tap = 0; tap < a.taps; ++tap) {
       float v[8];
+      const int s0 = a.a * t0 + a.beta + a.g * tap;  // input time of element 0
+      // interior unit-stride windows: two dwordx4 loads (dword alignment suffices; the tap shift
+      // makes most windows 16-byte unaligned); the rest element by element with masks
+      const bool interior = a.a == 1 && b < a.B && t0 + 7 < a.Tk && s0 >= 0 && s0 + 7 < a.Tv &&
+                            s0 + off >= 0 && s0 + 7 + off < Ts;
+      if (interior) {
+        const uint32_t vo = (uint32_t)(base + s0) * 4u;
+        const f32x4 lo = s1 ? ldb4(r1, vo) : ldb4(r0, vo);
+        const f32x4 hi = s1 ? ldb4(r1, vo + 16u) : ldb4(r0, vo + 16u);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int t = t0 + e;
-        const int tin = a.a * t + a.beta + a.g * tap;
-        const bool ok = b < a.B && t < a.Tk && (unsigned)tin < (unsigned)a.Tv &&
-                        (unsigned)(tin + off) < (unsigned)Ts;
-        const uint32_t vo = ok ? (uint32_t)(base + tin) * 4u : OOB;
-        v[e] = s1 ? ldb(r1, vo) : ldb(r0, vo);
+        for (int e = 0; e < 4; ++e) {
+          v[e] = lo[e];
+          v[e + 4] = hi[e];
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int t = t0 + e;
+          const int tin = s0 + a.a * e;
+          const bool ok = b < a.B && t < a.Tk && (unsigned)tin < (unsigned)a.Tv &&
+                          (unsigned)(tin + off) < (unsigned)Ts;
+          const uint32_t vo = ok ? (uint32_t)(base + tin) * 4u : OOB;
+          v[e] = s1 ? ldb(r1, vo) : ldb(r0, vo);
+        }
       }
       bf16x8 hi, mid, lo;
 #pragma unroll
@@ -1627,6 +1643,7 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
     b.T1 = d->src[1].T;
     b.off1 = d->src[1].off;
   }
+  MST_REQUIRE((long long)p.N * (Kp / 8) < (1ll << 31) && (long long)p.M * (Kp / 8) < (1ll << 31));
   for (const PackArgs* q : {&a, &b}) {  // 32-bit byte offsets through each source's descriptor
     const int C1 = q->rows / q->taps - q->C0;
     MST_REQUIRE((long long)(q->B - 1) * q->sb0 + (long long)(q->C0 - 1) * q->sc0 + q->T0 < (1ll << 29));

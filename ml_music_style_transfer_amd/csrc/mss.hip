@@ -433,7 +433,26 @@ __device__ __forceinline__ d2 twd(const d2* qt, int m, int N) {
   return dk(neg ? -a : a, neg ? -b : b);
 }
 
-// FB transforms of size N = 2^LOG2N in place in s[0 .. FB N) (Stockham, natural-order result)
+// LDS slot of complex element i of a wave buffer: an XOR-linear swizzle of the low 4 index bits
+// by bits 3..8, found by exhaustive local search over such swizzles against the bank rules of
+// ds_read_b128 (16-lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31}, 16 slots per 256-B row)
+// and ds_write_b128 (8 contiguous lanes, 8 slots per 128-B row) for every access of the loads,
+// the Stockham stages and the post-twist at n = 64 .. 2048 (model and search:
+// tools/lds_swizzle_search.py): 2604 -> 1004 modelled conflict cycles per wave pass; PMC before
+// it: 7.4 conflict cycles per LDS instruction (profiles/r05/pmc_mss_r5h_summary.txt).
+#ifndef MST_TSW
+#define MST_TSW 2  // A/B: 0 identity, 1 i ^ ((i >> 3) & 7) (1537 modelled cycles), 2 the searched one
+#endif
+__device__ __forceinline__ int tsw(int i) {
+  if constexpr (MST_TSW == 0) return i;
+  if constexpr (MST_TSW == 1) return i ^ ((i >> 3) & 7);
+  const int t = i >> 3;
+  const int b0 = t & 1, b12 = ((t >> 1) ^ (t >> 2)) & 1, b4 = (t >> 4) & 1, b5 = (t >> 5) & 1;
+  return i ^ (b0 ^ b5 ^ (-b12 & 15) ^ (-b4 & 9));
+}
+
+// FB transforms of size N = 2^LOG2N in place in s[0 .. FB N) (Stockham, natural-order result);
+// element i lives at slot tsw(i)
 template <int LOG2N, int BWT>
 __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
   constexpr int N = 1 << LOG2N, NR = N / 4, IT = BWT / 4 / 64;
@@ -445,7 +464,7 @@ __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
     for (int it = 0; it < IT; ++it) {
       const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[it][r] = s[fr * N + j + r * NR];
+      for (int r = 0; r < 4; ++r) v[it][r] = s[tsw(fr * N + j + r * NR)];
     }
     wave_sync();
 #pragma unroll
@@ -461,11 +480,11 @@ __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
       const d2 t0 = v[it][0] + v[it][2], t1 = v[it][0] - v[it][2];
       const d2 t2 = v[it][1] + v[it][3], t3 = v[it][1] - v[it][3];
       const d2 it3 = dk(-t3.y, t3.x);
-      d2* d = s + fr * N + (j - k) * 4 + k;
-      d[0] = t0 + t2;
-      d[Ns] = t1 - it3;
-      d[2 * Ns] = t0 - t2;
-      d[3 * Ns] = t1 + it3;
+      const int d = fr * N + (j - k) * 4 + k;
+      s[tsw(d)] = t0 + t2;
+      s[tsw(d + Ns)] = t1 - it3;
+      s[tsw(d + 2 * Ns)] = t0 - t2;
+      s[tsw(d + 3 * Ns)] = t1 + it3;
     }
     wave_sync();
     Ns *= 4;
@@ -476,8 +495,8 @@ __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
 #pragma unroll
     for (int it = 0; it < IT2; ++it) {
       const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
-      v[it][0] = s[fr * N + j];
-      v[it][1] = s[fr * N + j + NR2];
+      v[it][0] = s[tsw(fr * N + j)];
+      v[it][1] = s[tsw(fr * N + j + NR2)];
     }
     wave_sync();
 #pragma unroll
@@ -485,9 +504,9 @@ __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
       const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
       const int k = j & (Ns - 1);
       const d2 b = dmul(v[it][1], twd(qt, k, 2 * Ns));
-      d2* d = s + fr * N + (j - k) * 2 + k;
-      d[0] = v[it][0] + b;
-      d[Ns] = v[it][0] - b;
+      const int d = fr * N + (j - k) * 2 + k;
+      s[tsw(d)] = v[it][0] + b;
+      s[tsw(d + Ns)] = v[it][0] - b;
     }
     wave_sync();
   }
@@ -496,7 +515,10 @@ __device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
 constexpr int MSS_TW = 4;           // waves per target workgroup
 constexpr int MSS_TBW = 512;        // complex doubles per wave buffer (n/2 <= 512); n = 2048: 1024
 constexpr int MSS_TROUNDS = 4;      // frame batches per wave per workgroup
-constexpr int MSS_TLDS = MSS_TW * 1024 * 16 + 512 * 16;  // wave buffers (n = 2048 size) + table
+// LDS: wave buffers + the twiddle table; n <= 1024 (40 KB, three workgroups per CU) and n = 2048
+// (72 KB, two) run as separate launches so the small sizes are not held to the large size's LDS
+template <bool BIG>
+constexpr int mss_tlds() { return MSS_TW * (BIG ? 1024 : 512) * 16 + 512 * 16; }
 
 struct MssTgt {
   const float* target;
@@ -513,7 +535,7 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
   constexpr int FBT = BWT / HALF;            // frames per wave batch
   constexpr int NEO = (FBT * NBIN + 63) / 64;  // output bins per lane
   d2* qt = reinterpret_cast<d2*>(lds);
-  d2* S = qt + 512 + (threadIdx.x >> 6) * 1024;
+  d2* S = qt + 512 + (threadIdx.x >> 6) * BWT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int r = threadIdx.x; r < 512; r += 256) {
     const double2 w = kMssW2048d.w[r];
@@ -546,7 +568,7 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
       const int e = lane + 64 * kk, u = e / HALF, j = e - u * HALF;
       const d2 c0 = twd(qt, 2 * j, N), c1 = twd(qt, 2 * j + 1, N);  // W_N^k: cos(2 pi k / N)
       const double w0 = 0.5 - 0.5 * c0.x, w1 = 0.5 - 0.5 * c1.x;
-      S[e] = dk(w0 * (double)xa[kk], w1 * (double)xb[kk]);
+      S[tsw(e)] = dk(w0 * (double)xa[kk], w1 * (double)xb[kk]);
     }
     wave_sync();
     wave_fft_d<LOG2N - 1, BWT>(S, qt, lane);
@@ -556,8 +578,7 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
       const int e = lane + 64 * jj, m = e / NBIN, f = e - m * NBIN;
       const int t = t0 + m;
       if (e < FBT * NBIN && t < T) {
-        const d2* Z = S + m * HALF;
-        const d2 Af = Z[f & (HALF - 1)], Bf = Z[(HALF - f) & (HALF - 1)];
+        const d2 Af = S[tsw(m * HALF + (f & (HALF - 1)))], Bf = S[tsw(m * HALF + ((HALF - f) & (HALF - 1)))];
         const d2 E = dk(0.5 * (Af.x + Bf.x), 0.5 * (Af.y - Bf.y));
         const d2 D = dk(0.5 * (Af.y + Bf.y), -0.5 * (Af.x - Bf.x));  // -i (A - conj B) / 2
         const d2 X = E + dmul(twd(qt, f, N), D);
@@ -568,9 +589,9 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
   }
 }
 
-// grid (max nblk, B, sizes); every size of the call in one launch
-__global__ __launch_bounds__(256, 2) void mss_target_kernel(const MssTgt A) {
-  __shared__ __attribute__((aligned(16))) char lds[MSS_TLDS];
+// grid (max nblk, B, sizes of the launch): n = 64 .. 1024 in one launch, n = 2048 in another
+__global__ __launch_bounds__(256, 3) void mss_target_kernel(const MssTgt A) {
+  __shared__ __attribute__((aligned(16))) char lds[mss_tlds<false>()];
   const int z = blockIdx.z, blk = blockIdx.x, b = blockIdx.y;
   if (blk >= A.nblk[z]) return;
   switch (A.lg[z]) {
@@ -578,9 +599,14 @@ __global__ __launch_bounds__(256, 2) void mss_target_kernel(const MssTgt A) {
     case 7: mss_target_body<7>(A, z, blk, b, lds); break;
     case 8: mss_target_body<8>(A, z, blk, b, lds); break;
     case 9: mss_target_body<9>(A, z, blk, b, lds); break;
-    case 10: mss_target_body<10>(A, z, blk, b, lds); break;
-    default: mss_target_body<11>(A, z, blk, b, lds); break;
+    default: mss_target_body<10>(A, z, blk, b, lds); break;
   }
+}
+__global__ __launch_bounds__(256, 2) void mss_target2048_kernel(const MssTgt A) {
+  __shared__ __attribute__((aligned(16))) char lds[mss_tlds<true>()];
+  const int blk = blockIdx.x, b = blockIdx.y;
+  if (blk >= A.nblk[0]) return;
+  mss_target_body<11>(A, 0, blk, b, lds);
 }
 
 int mss_target_frames_per_wg(int lg) {
@@ -797,21 +823,30 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
   hipStream_t st = (hipStream_t)stream;
   float* w = (float*)ws;
   MST_REQUIRE(((uintptr_t)ws & 15) == 0);
-  // the target's magnitudes, every size in one launch
-  MssTgt tg;
-  tg.target = target;
-  tg.L = L;
-  tg.nsz = pl.nsz;
-  unsigned max_blk = 0;
-  for (int s = 0; s < pl.nsz; ++s) {
-    tg.lg[s] = log2i(pl.n[s]);
-    tg.T[s] = pl.T[s];
-    tg.nblk[s] = ceil_div(pl.T[s], mss_target_frames_per_wg(tg.lg[s]));
-    tg.tmag[s] = w + pl.tmag_off[s];
-    max_blk = max_blk > (unsigned)tg.nblk[s] ? max_blk : (unsigned)tg.nblk[s];
+  // the target's magnitudes: n = 64 .. 1024 in one launch, n = 2048 in another
+  MssTgt tg[2];
+  unsigned max_blk[2] = {0, 0};
+  for (int k = 0; k < 2; ++k) {
+    tg[k].target = target;
+    tg[k].L = L;
+    tg[k].nsz = 0;
   }
-  hipLaunchKernelGGL(mss_target_kernel, dim3(max_blk, (unsigned)B, (unsigned)pl.nsz), dim3(256), 0, st, tg);
-  MST_CHECK_LAUNCH();
+  for (int s = 0; s < pl.nsz; ++s) {
+    const int lg = log2i(pl.n[s]), k = lg == 11 ? 1 : 0, z = tg[k].nsz++;
+    tg[k].lg[z] = lg;
+    tg[k].T[z] = pl.T[s];
+    tg[k].nblk[z] = ceil_div(pl.T[s], mss_target_frames_per_wg(lg));
+    tg[k].tmag[z] = w + pl.tmag_off[s];
+    max_blk[k] = max_blk[k] > (unsigned)tg[k].nblk[z] ? max_blk[k] : (unsigned)tg[k].nblk[z];
+  }
+  if (tg[0].nsz > 0) {
+    hipLaunchKernelGGL(mss_target_kernel, dim3(max_blk[0], (unsigned)B, (unsigned)tg[0].nsz), dim3(256), 0, st, tg[0]);
+    MST_CHECK_LAUNCH();
+  }
+  if (tg[1].nsz > 0) {
+    hipLaunchKernelGGL(mss_target2048_kernel, dim3(max_blk[1], (unsigned)B, 1), dim3(256), 0, st, tg[1]);
+    MST_CHECK_LAUNCH();
+  }
   MssMulti mm;
   mm.nsz = 0;
   unsigned max_nwg = 0;

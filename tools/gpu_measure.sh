@@ -26,6 +26,8 @@ for what in "$@"; do
       timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
         --output-format csv -d "$OUT/pmcgemm/p1" -o run -- \
         python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0 > "$OUT/pmcgemm.log" 2>&1 ;;
+    pmcmss2)
+      bash tools/pmc_cmd.sh "$OUT/pmcmss2" bench_aux.py --workload mss --no-cpu-baseline --no-parity --steps 2 --warmup 1 ;;
     pmcall)  # FETCH / WRITE passes over the bench step and over each aux leg (traffic JSONs)
       for w in step frontend griffinlim mss; do
         if [ $w = step ]; then cmd="bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-aux --kernel-timing-steps 0";
