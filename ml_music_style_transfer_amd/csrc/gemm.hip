@@ -935,6 +935,86 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
     const int Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
     const int k0 = 8 * kq, b = k0 / a.Tp, t0 = k0 - b * a.Tp;
     const int base = b * (int)(s1 ? a.sb1 : a.sb0) + cs * (s1 ? a.sc1 : a.sc0) + off;
+    if (a.a == 1 && a.Tv <= a.Tp &&
+        (a.taps == 1 ? a.g == 0 && a.beta == 0 : a.g == 1 && a.beta == -1 && a.taps == 3)) {
+      // unit-stride rows (k3 convolutions, taps 3; and the P operand, taps 1): branch-free.
+      // Each lane loads ITS OWN 8 elements u = t0 .. t0 + 7 with two dwordx4 loads (dword
+      // alignment suffices), out-of-range elements zeroed by selects; a k3 tap window
+      // u = t0 - 1 + tap + e takes its two halo elements from the neighbouring lanes (the previous
+      // / next 8 k: across a batch-row or channel boundary the halo element is out of range anyway,
+      // as Tv <= Tp),
+      // the wave's first / last lane from two extra masked loads. Each element is split once.
+      const bool rowok = b < a.B;
+      const int u0 = t0;
+      // the 8 own elements, valid where u < Tv and u + off inside the source; the dwordx4 pair is
+      // used where it lies inside the source buffer (the descriptor's extent)
+      const long long ext = s1 ? (long long)(a.B - 1) * a.sb1 + (long long)(chans - a.C0 - 1) * a.sc1 + a.T1
+                               : (long long)(a.B - 1) * a.sb0 + (long long)(a.C0 - 1) * a.sc0 + a.T0;
+      const bool vec = base + u0 >= 0 && (long long)base + u0 + 8 <= ext;
+      float own[8];
+      {
+        const uint32_t vo = (uint32_t)(base + u0) * 4u;
+        const uint32_t v0 = vec ? vo : OOB, v1 = vec ? vo + 16u : OOB;
+        const f32x4 lo = s1 ? ldb4(r1, v0) : ldb4(r0, v0);
+        const f32x4 hi = s1 ? ldb4(r1, v1) : ldb4(r0, v1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          own[e] = lo[e];
+          own[e + 4] = hi[e];
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int u = u0 + e;
+        const bool ok = rowok && (unsigned)u < (unsigned)a.Tv && (unsigned)(u + off) < (unsigned)Ts;
+        if (!vec) {  // the rare lane whose pair would leave the buffer: element by element
+          own[e] = s1 ? ldb(r1, ok ? (uint32_t)(base + u) * 4u : OOB) : ldb(r0, ok ? (uint32_t)(base + u) * 4u : OOB);
+        }
+        own[e] = ok ? own[e] : 0.f;
+      }
+      const int lane = threadIdx.x & 63;
+      const int ntap = a.taps;
+      float hl = 0.f, hr = 0.f;  // u = t0 - 1 and u = t0 + 8
+      if (ntap == 3) {
+        hl = __shfl_up(own[7], 1, 64);
+        hr = __shfl_down(own[0], 1, 64);
+        // wave edges: the neighbour item belongs to another wave; load the element itself
+        const int ul = u0 - 1, ur = u0 + 8;
+        const bool okl = lane == 0 && rowok && (unsigned)ul < (unsigned)a.Tv && (unsigned)(ul + off) < (unsigned)Ts;
+        const bool okr = lane == 63 && rowok && (unsigned)ur < (unsigned)a.Tv && (unsigned)(ur + off) < (unsigned)Ts;
+        const float el = s1 ? ldb(r1, okl ? (uint32_t)(base + ul) * 4u : OOB) : ldb(r0, okl ? (uint32_t)(base + ul) * 4u : OOB);
+        const float er = s1 ? ldb(r1, okr ? (uint32_t)(base + ur) * 4u : OOB) : ldb(r0, okr ? (uint32_t)(base + ur) * 4u : OOB);
+        // a halo element is valid only inside this row (t0 > 0 / t0 + 8 < Tv) and the source
+        const bool vl = rowok && t0 > 0 && (unsigned)(ul + off) < (unsigned)Ts && ul < a.Tv;
+        const bool vr = rowok && (unsigned)ur < (unsigned)a.Tv && (unsigned)(ur + off) < (unsigned)Ts;
+        hl = lane == 0 ? el : (vl ? hl : 0.f);
+        hr = lane == 63 ? er : (vr ? hr : 0.f);
+      }
+      Bf3 sp[10];
+      sp[0] = split1(hl);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sp[e + 1] = split1(own[e]);
+      sp[9] = split1(hr);
+#pragma unroll
+      for (int tap = 0; tap < 3; ++tap) {  // unrolled: sp[] stays in registers
+        if (tap >= ntap) break;
+        bf16x8 hi, mid, lo;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const bool ok = t0 + e < a.Tk;  // time padding
+          // taps 3: window element e + tap (u = t0 - 1 + tap + e); taps 1: own element e
+          const Bf3 v = ntap == 3 ? sp[e + tap] : sp[e + 1];
+          hi[e] = ok ? v.h : (__bf16)0.f;
+          mid[e] = ok ? v.m : (__bf16)0.f;
+          lo[e] = ok ? v.l : (__bf16)0.f;
+        }
+        __bf16* o = a.out + (long long)(c * ntap + tap) * a.ld + k0;
+        *reinterpret_cast<bf16x8*>(o) = hi;
+        *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
+        *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
+      }
+      continue;
+    }
     for (int tap = 0; tap < a.taps; ++tap) {
       float v[8];
       const int s0 = a.a * t0 + a.beta + a.g * tap;  // input time of element 0
