@@ -180,7 +180,7 @@ def gemm_traffic():
 
 def gemm_pmc():
     """MFMA-busy and VALU:MFMA per GEMM kind from the newest round's committed PMC summary
-    (profiles/r*/gemm_pmc.json: tools/pmc_gemm.py over rocprofv3 --pmc passes of this bench)."""
+    (profiles/r*/gemm_pmc.json: tools/pmc_gemm_json.py over rocprofv3 --pmc passes of this bench)."""
     pdir = os.path.join(ROOT, "profiles")
     rounds = sorted((d for d in os.listdir(pdir) if d.startswith("r")), reverse=True) \
         if os.path.isdir(pdir) else []
@@ -189,8 +189,9 @@ def gemm_pmc():
         if os.path.exists(pj):
             with open(pj) as fh:
                 d = json.load(fh)
-            d["source"] = f"profiles/{r}/gemm_pmc.json"
-            return d
+            return {"build": d.get("build"), "source": f"profiles/{r}/gemm_pmc.json",
+                    "kinds": {k: {x: y for x, y in e.items() if x != "counters"}
+                              for k, e in d.get("kinds", {}).items()}}
     return None
 
 
@@ -418,8 +419,9 @@ def main():
                    "sample_rate": SR, "n_fft": 2048, "hop": HOP, "parallelism": f"dp{world}"},
         "roofline": {
             "bound": "mfma",
-            "kernel": ("gemm_w_kernel (128 x 256 tiles: conv/linear fwd and dgrad) and gemm_kernel "
-                       "(128 x 128: wgrad, stream-K) (implicit GEMM; fp32 operands "
+            "kernel": ("gemm_w_kernel (128 x 256 tiles: conv/linear fwd and dgrad, operands split in "
+                       "registers) and gemm_p_kernel (128 x 256: wgrad on operand planes pre-split by "
+                       "pack_planes_kernel, split-K) (implicit GEMM; fp32 operands "
                        + ("split into 3 bf16 pieces, 6 x v_mfma_f32_32x32x16_bf16 per 16-deep k step)"
                           if products > 1 else "v_mfma_f32_32x32x2_f32)")),
             "achieved": round(achieved, 2),
