@@ -204,6 +204,21 @@ def test_gemm_stream_k(cuda, sched):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("splitk", [2, 5, 16])
+def test_splitk_fixup_handoff(cuda, splitk):
+    """The opt-in in-GEMM split-K fixup (MST_SPLITK_FIXUP=1, read once per process: run in a child,
+    tests/_fixup_child.py): float64 parity and bitwise repeatability under a concurrent stream."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "_fixup_child.py"), str(splitk)],
+                       env=dict(os.environ, MST_SPLITK_FIXUP="1"), cwd=root, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "fixup ok" in r.stdout, r.stdout[-2000:]
+
+
 @pytest.mark.parametrize("B", [2, 32])
 def test_conv3_concat_sources_and_split_dsts(cuda, B):
     """Virtual concat with a time offset (crop_and_concat) and a split dgrad destination."""
