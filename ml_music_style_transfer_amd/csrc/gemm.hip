@@ -215,6 +215,7 @@ struct GP {
   unsigned long long* cnt;
   unsigned long long tag;
   int fixup;
+  int slab4;  // split-K slabs stored as dwordx4 rows (N % 4 == 0, M N < 2^29; store_slab4)
 };
 
 // Tile-order index -> (M tile, N tile): runs of GM M-tiles x all N-tiles, M fastest within a
@@ -687,6 +688,27 @@ static_assert(BM * BNW <= LDS_W_FLOATS, "epilogue tile must fit the two stages")
 // last arrival clears its word, since graph replays reuse a launch's tag.
 constexpr int SC1 = 16;  // buffer instruction cache policy: sc1 (write-through / L2-bypassing read)
 
+// Split-K slab of a 128 x 256 tile from the LDS tile: one dwordx4 per thread per row, 16 row
+// passes with 32-bit offsets (the per-element stores did 64-bit index math for every element:
+// the weight-gradient kernels' short-K splits spent more VALU in that epilogue than in their
+// main loops, PMC VALU:MFMA 2.3 against 0.33 in the loop).
+__device__ __forceinline__ void store_slab4(const GP& p, const float* Cs, int m0, int n0, int split,
+                                            int tid) {
+  constexpr int Q = BNW / 4, RPP = NTHRW / Q;
+  const long long MN = (long long)p.M * p.N;
+  const int q = tid & (Q - 1), r0 = tid / Q;
+  const int n = n0 + 4 * q;
+  const rsrc_t rs = mk_rsrc(p.ws + split * MN, MN);
+  const int nrow = p.M - m0 < BM ? p.M - m0 : BM;
+#pragma unroll
+  for (int i = 0; i < BM / RPP; ++i) {
+    const int ml = r0 + RPP * i;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(Cs + ml * BNW + 4 * q);
+    const uint32_t vo = (ml < nrow && n < p.N) ? (uint32_t)((m0 + ml) * p.N + n) * 4u : OOB;
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)vo, 0, 0);
+  }
+}
+
 template <bool WG>
 __device__ __forceinline__ void splitk_epilogue(const GP& p, const float* Cs, int m0, int n0, int split,
                                                 int tile, int tid) {
@@ -940,6 +962,10 @@ __device__ __forceinline__ void tile_pass_w(const GP& p, float* lds, int m_t, in
   __syncthreads();
   if (p.fixup) {
     splitk_epilogue<false>(p, Cs, m_t * BM, n_t * BNW, split, m_t * ((p.N + BNW - 1) / BNW) + n_t, tid);
+    return;
+  }
+  if (p.slab4) {
+    store_slab4(p, Cs, m_t * BM, n_t * BNW, split, tid);
     return;
   }
   if (n < p.N) {
@@ -1248,6 +1274,10 @@ __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int
     splitk_epilogue<WG>(p, Cs, m0, n0, split, m_t * ((p.N + BNW - 1) / BNW) + n_t, tid);
     return;
   }
+  if (p.slab4) {
+    store_slab4(p, Cs, m0, n0, split, tid);
+    return;
+  }
   const int nl = tid & (BNW - 1);
   const int n = n0 + nl;
   if (n < p.N) {
@@ -1519,6 +1549,14 @@ bool fixup_ok(int M, int N, int splitk) {
          (long long)M * N < (1ll << 29);
 }
 
+bool slab4_ok(int M, int N, int splitk) {  // MST_SLAB4=0: per-element slab stores (A/B)
+  static const int env = [] {
+    const char* e = getenv("MST_SLAB4");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return env && splitk > 1 && N % 4 == 0 && (long long)M * N < (1ll << 29);
+}
+
 size_t fixup_cnt_bytes(int M, int N) {  // one 64-bit arrival counter per 128 x 256 tile
   return (size_t)ceil_div(M, BM) * ceil_div(N, BNW) * sizeof(unsigned long long);
 }
@@ -1554,6 +1592,7 @@ void bind_ws(GP& p, float* ws, size_t ws_bytes) {
   }
   p.ws = ws;
   p.fixup = 0;
+  p.slab4 = p.wide && p.sk_L == 0 && slab4_ok(p.M, p.N, p.splitk);
   if (wide_fixup(p)) {
     p.fixup = 1;
     p.cnt = reinterpret_cast<unsigned long long*>(
@@ -1886,6 +1925,7 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
   w.a_bytes = round256((size_t)(3 * p.psa) * 2);
   w.b_bytes = round256((size_t)(3 * p.psb) * 2);
   p.fixup = fixup_ok(p.M, p.N, p.splitk) ? 1 : 0;
+  p.slab4 = slab4_ok(p.M, p.N, p.splitk) ? 1 : 0;
   w.cnt_bytes = p.fixup ? round256(fixup_cnt_bytes(p.M, p.N)) : 0;
   return MST_OK;
 }
