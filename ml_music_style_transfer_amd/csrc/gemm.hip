@@ -240,10 +240,8 @@ __device__ __forceinline__ int xcd_order(int w, int W) {
 
 // bias value bm = p.bias[m] passed in (loaded ahead by the caller: a load inside this per-element
 // path, behind its branches, makes the compiler wait for it element by element)
-__device__ __forceinline__ void conv_store_b(const GP& p, int m, int n, float v, float bm) {
-  if (m >= p.M || n >= p.N) return;
-  int b = n / p.Tn;
-  int t = n - b * p.Tn;
+// element (m, n = b Tn + t) with (b, t) known
+__device__ __forceinline__ void conv_store_bt(const GP& p, int m, int b, int t, float v, float bm) {
   v *= p.alpha;
   if (p.bias) v += bm;
   if (p.act == MST_ACT_RELU) v = fmaxf(v, 0.f);
@@ -268,6 +266,12 @@ __device__ __forceinline__ void conv_store_b(const GP& p, int m, int n, float v,
     if (p.gt1) v = p.gt1[idx] > 0.f ? v * p.gs1 : 0.f;
     p.y1[idx] = v;
   }
+}
+
+__device__ __forceinline__ void conv_store_b(const GP& p, int m, int n, float v, float bm) {
+  if (m >= p.M || n >= p.N) return;
+  const int b = n / p.Tn;
+  conv_store_bt(p, m, b, n - b * p.Tn, v, bm);
 }
 
 __device__ __forceinline__ void conv_store(const GP& p, int m, int n, float v) {
@@ -1448,6 +1452,61 @@ __global__ __launch_bounds__(256) void splitk_reduce4_kernel(const GP p) {
   }
 }
 
+// The same reduction by rows (N % 4 == 0): grid (ceil(N/4 / 64), ceil(M / 4)), one wave per row m
+// and 64 column quads, so m and n need no division; one division per thread for the conv
+// epilogue's (b, t), then t steps through the quad. Slabs summed in split order (bitwise the
+// kernels above).
+template <bool WG>
+__global__ __launch_bounds__(256) void splitk_reduce_rows_kernel(const GP p) {
+  const int m = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int n = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4;
+  if (m >= p.M || n >= p.N) return;
+  const long long MN = (long long)p.M * p.N;
+  const float* w = p.ws + (long long)m * p.N + n;
+  f32x4 v = *reinterpret_cast<const f32x4*>(w);
+  for (int s = 1; s < p.splitk; ++s) v += *reinterpret_cast<const f32x4*>(w + s * MN);
+  if constexpr (WG) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wgrad_store(p, m, n + e, v[e]);
+  } else {
+    const float bm = p.bias ? p.bias[m] : 0.f;
+    int b = n / p.Tn, t = n - b * p.Tn;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      conv_store_bt(p, m, b, t, v[e], bm);
+      if (++t == p.Tn) {
+        t = 0;
+        ++b;
+      }
+    }
+  }
+}
+
+static int reduce_rows() {  // MST_REDUCE_ROWS=0: the 1-D float4 reduce (A/B)
+  static const int v = [] {
+    const char* e = getenv("MST_REDUCE_ROWS");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+template <bool WG>
+void launch_reduce(const GP& p, hipStream_t st) {
+  const long long total = (long long)p.M * p.N;
+  if (reduce_rows() && p.N % 4 == 0 && p.M < 65535 * 4) {
+    hipLaunchKernelGGL((splitk_reduce_rows_kernel<WG>), dim3(ceil_div(p.N / 4, 64), ceil_div(p.M, 4)),
+                       dim3(256), 0, st, p);
+  } else if (total % 4 == 0 && total < (1ll << 31)) {
+    int blocks = (int)((total / 4 + 255) / 256);
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL((splitk_reduce4_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+  } else {
+    int blocks = (int)((total + 255) / 256);
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL((splitk_reduce_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
+  }
+}
+
 // Split-K from a wave-quantisation cost model. 256 CUs x occ resident workgroups = the slots;
 // a workgroup's time is ~ (its K tiles) x tau. At occ = 2 a trailing partial wave of <= 256
 // workgroups runs one workgroup per CU (no MFMA-pipe sharing) and costs ~0.55 of a full wave;
@@ -1646,16 +1705,7 @@ int launch(const GP& p, hipStream_t st, int taps) {
     MST_CHECK_LAUNCH();
   }
   if (p.splitk > 1 && !p.fixup) {
-    long long total = (long long)p.M * p.N;
-    if (total % 4 == 0 && total < (1ll << 31)) {
-      int blocks = (int)((total / 4 + 255) / 256);
-      if (blocks > 8192) blocks = 8192;
-      hipLaunchKernelGGL((splitk_reduce4_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
-    } else {
-      int blocks = (int)((total + 255) / 256);
-      if (blocks > 4096) blocks = 4096;
-      hipLaunchKernelGGL((splitk_reduce_kernel<WG>), dim3(blocks), dim3(256), 0, st, p);
-    }
+    launch_reduce<WG>(p, st);
     MST_CHECK_LAUNCH();
   }
   return MST_OK;
@@ -1959,16 +2009,7 @@ int run_wgrad_planes(PlanesWG& w, float* ws, hipStream_t st) {
   hipLaunchKernelGGL((gemm_p_kernel<true>), grid, dim3(NTHRW), 0, st, p);
   MST_CHECK_LAUNCH();
   if (p.splitk > 1 && !p.fixup) {
-    const long long total = (long long)p.M * p.N;
-    if (total % 4 == 0 && total < (1ll << 31)) {
-      int blocks = (int)((total / 4 + 255) / 256);
-      if (blocks > 8192) blocks = 8192;
-      hipLaunchKernelGGL((splitk_reduce4_kernel<true>), dim3(blocks), dim3(256), 0, st, p);
-    } else {
-      int blocks = (int)((total + 255) / 256);
-      if (blocks > 4096) blocks = 4096;
-      hipLaunchKernelGGL((splitk_reduce_kernel<true>), dim3(blocks), dim3(256), 0, st, p);
-    }
+    launch_reduce<true>(p, st);
     MST_CHECK_LAUNCH();
   }
   return MST_OK;
