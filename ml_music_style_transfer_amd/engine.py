@@ -50,8 +50,9 @@ class GradSink:
     input gradient), so with a side stream (`side`) they run there, concurrently with the
     input-gradient GEMMs and norm kernels of the main stream: a GEMM's trailing partial wave of
     workgroups no longer leaves the chip half idle. Tensors a side launch reads are recorded on
-    the side stream (the caching allocator must not hand them out again before it is done), and
-    the main stream waits for the side stream before the block listeners run and at the end.
+    the side stream (the caching allocator must not hand them out again before it is done). The
+    block listeners run with the side stream current (after it has waited for the main stream),
+    and the main stream waits for the side stream only at the end.
     `joined` is the event the main stream last waited on: it completes with the last side-stream
     launch (the side stream may still carry the caching allocator's free markers behind it,
     which are events, not work)."""
@@ -97,8 +98,17 @@ class GradSink:
 
     def block_done(self):
         if self.on_ready is not None and self._pending:
-            self.join()
-            self.on_ready(self._pending)
+            if self.side is not None:
+                # the listeners issue from the weight-gradient stream, which first waits for the
+                # main stream up to this point: their collectives / updates then follow both
+                # streams' gradient kernels, and the main stream never waits for the weight
+                # gradients inside backward (joining it here, as rounds 1-4 did, serialised the
+                # two streams at every block whenever a DP reducer or BackwardAdam was attached)
+                self.side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(self.side):
+                    self.on_ready(self._pending)
+            else:
+                self.on_ready(self._pending)
         self._pending = []
 
 
