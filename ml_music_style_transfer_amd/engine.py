@@ -57,13 +57,18 @@ class GradSink:
     launch (the side stream may still carry the caching allocator's free markers behind it,
     which are events, not work)."""
 
-    def __init__(self, flat_grad_of=None, on_ready=None, side=None):
+    def __init__(self, flat_grad_of=None, on_ready=None, side=None, main_tail=0, blocks=None):
         self.flat_grad_of = flat_grad_of or (lambda p: None)
         self.on_ready = on_ready
         self.side = side
         self._side_pending = False
         self._pending = []
         self.joined = None
+        # the weight gradients of the last `main_tail` blocks (of `blocks` in the previous
+        # backward) run on the main stream: once the main stream's input gradients are done the
+        # side stream still holds a backlog, so both streams then carry weight gradients
+        self.block = 0
+        self._main_from = blocks - main_tail if (blocks is not None and main_tail > 0) else None
 
     def target(self, p):
         self._pending.append(p)
@@ -77,7 +82,7 @@ class GradSink:
 
     def wgrad(self, launch, *reads):
         """Run a weight-gradient launch (on the side stream when there is one)."""
-        if self.side is None:
+        if self.side is None or (self._main_from is not None and self.block >= self._main_from):
             launch()
             return
         main = torch.cuda.current_stream()
@@ -110,6 +115,7 @@ class GradSink:
             else:
                 self.on_ready(self._pending)
         self._pending = []
+        self.block += 1
 
 
 # ------------------------------------------------------------------ DownConv
@@ -445,6 +451,7 @@ class PerformanceNetFunction(torch.autograd.Function):
         # the side stream's join event (None when the weight gradients ran on the compute
         # stream): an Event, so no hook closure of this backward outlives it
         module.__dict__["_mst_wgrad_joined"] = sink.joined
+        module.__dict__["_mst_bwd_blocks"] = sink.block
         for h in hooks:
             h.launch_remaining()
         ctx.state = None

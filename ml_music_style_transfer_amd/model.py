@@ -54,6 +54,8 @@ def slot_view(buf, p):
 # set_wgrad_stream(False) does too (bench.py's per-launch timing leg: overlapping kernels
 # would make per-launch times meaningless). Stream capture (graphs.py) always runs serially.
 _WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "1") == "1"
+# the last N backward blocks' weight gradients on the main stream (engine.GradSink); A/B knob
+_WGRAD_MAIN_TAIL = int(os.environ.get("MST_WGRAD_MAIN_TAIL", "2"))
 
 
 def set_wgrad_stream(on):
@@ -416,7 +418,8 @@ class PerformanceNet(nn.Module):
             side = self.__dict__.get("_mst_side")
             if side is None or side.device != dev:
                 side = self.__dict__["_mst_side"] = torch.cuda.Stream(device=dev)
-        return E.GradSink(flat_grad_of, on_ready, side)
+        return E.GradSink(flat_grad_of, on_ready, side, _WGRAD_MAIN_TAIL,
+                          self.__dict__.get("_mst_bwd_blocks"))
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
