@@ -288,21 +288,44 @@ DN = ("fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias")
 UP = ("upconv.weight", "upconv.bias", "conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias")
 
 
-def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5, seed_dev=None):
+def _record(obj, stream):
+    """record_stream(stream) on every tensor of a nested tuple / list: tensors made on one stream
+    and used on another must not be handed out again by the caching allocator before the other
+    stream's kernels are done with them."""
+    if isinstance(obj, torch.Tensor):
+        obj.record_stream(stream)
+    elif isinstance(obj, (list, tuple)):
+        for o in obj:
+            _record(o, stream)
+
+
+def _encoder_fwd(P, name, x, depth, enc, svs):
+    for i in range(depth):
+        x, before, sv = downconv_fwd(*_pp(P, f"{name}.{i}", DC), x, i < depth - 1)
+        enc.append(before)
+        svs.append(sv)
+    return x
+
+
+def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5, seed_dev=None, aux=None):
     """PerformanceNet.forward (model.py:262-300) as one kernel program. seed_dev (optional
-    int64 device scalar) is added to every dropout seed on the device (hipGraph replays)."""
+    int64 device scalar) is added to every dropout seed on the device (hipGraph replays).
+
+    aux (optional stream): the audio encoder runs on it, concurrently with the MIDI and
+    onset/offset encoders on the current stream (independent branches until dense_concats.0;
+    their deep levels are a few hundred workgroups each, so one alone leaves the chip idle).
+    Same kernels, same results."""
     enc_m, enc_a, sv_m, sv_a = [], [], [], []
-    xm = x_midi
-    for i in range(depth):
-        xm, before, sv = downconv_fwd(*_pp(P, f"down_convs.{i}", DC), xm, i < depth - 1)
-        enc_m.append(before)
-        sv_m.append(sv)
-    xa = x_audio
-    for i in range(depth):
-        xa, before, sv = downconv_fwd(*_pp(P, f"down_convs_audio.{i}", DC), xa, i < depth - 1)
-        enc_a.append(before)
-        sv_a.append(sv)
-    x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed, seed_dev)
+    main = torch.cuda.current_stream()
+    if aux is not None:
+        aux.wait_stream(main)
+        x_audio.record_stream(aux)
+    xm = _encoder_fwd(P, "down_convs", x_midi, depth, enc_m, sv_m)
+    if aux is not None:
+        with torch.cuda.stream(aux):
+            xa = _encoder_fwd(P, "down_convs_audio", x_audio, depth, enc_a, sv_a)
+    else:
+        xa = _encoder_fwd(P, "down_convs_audio", x_audio, depth, enc_a, sv_a)
     conds, sv_o = [], []
     c = cond
     for i in range(3):
@@ -310,6 +333,10 @@ def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5, seed_dev=
         sv_o.append(sv)
         if i > 0:
             conds.append(c)
+    if aux is not None:
+        main.wait_stream(aux)
+        _record((xa, enc_a, sv_a), main)
+    x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed, seed_dev)
     sv_dn, sv_up = [], []
     for i in range(4):
         skip, svd = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
@@ -344,7 +371,7 @@ def backward_param_order(depth=5):
     return names
 
 
-def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
+def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False), aux=None):
     depth = st["depth"]
     y = st["y"]
     dypre = K.lrelu_bwd(dy, y)
@@ -395,9 +422,7 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
                              d_pool0=d1, need_dx=need_input_grads[2])
     sink.block_done()
     del d1
-    grads_in = []
-    for name, sv, d_before, d_top in (("down_convs", st["sv_m"], d_before_m, d_xm),
-                                      ("down_convs_audio", st["sv_a"], d_before_a, d_xa)):
+    def encoder_bwd(name, sv, d_before, d_top):
         d_pool = None
         for i in reversed(range(depth)):
             prm = _pp(P, f"{name}.{i}", DC)
@@ -410,9 +435,24 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False)):
                                       need_dx=need)
             sink.block_done()
             d_before[i] = None
-        grads_in.append(d_pool)
+        return d_pool
+
+    # the two encoders' backward are independent: with an aux stream the audio encoder's runs on
+    # it beside the MIDI encoder's (enqueued second, so blocks finish in the flat-buffer order)
+    main = torch.cuda.current_stream()
+    g_m = encoder_bwd("down_convs", st["sv_m"], d_before_m, d_xm)
+    if aux is not None:
+        aux.wait_stream(main)
+        _record((d_before_a, d_xa, st["sv_a"]), aux)
+        with torch.cuda.stream(aux):
+            g_a = encoder_bwd("down_convs_audio", st["sv_a"], d_before_a, d_xa)
+        main.wait_stream(aux)
+        if g_a is not None:
+            g_a.record_stream(main)
+    else:
+        g_a = encoder_bwd("down_convs_audio", st["sv_a"], d_before_a, d_xa)
     sink.join()
-    return grads_in[0], grads_in[1], d_cond_in
+    return g_m, g_a, d_cond_in
 
 
 class PerformanceNetFunction(torch.autograd.Function):
@@ -426,7 +466,8 @@ class PerformanceNetFunction(torch.autograd.Function):
         xm, xa, cd = (t if t.stride(2) == 1 and t.dtype == torch.float32 else t.float().contiguous()
                       for t in (x_midi, x_audio, cond))
         y, state = network_fwd(P, xm, xa, cd, drop_p, seed, module.depth,
-                               module.__dict__.get("_mst_seed_dev") if drop_p > 0 else None)
+                               module.__dict__.get("_mst_seed_dev") if drop_p > 0 else None,
+                               aux=module._enc_stream())
         ctx.module = module
         ctx.state = state
         return y
@@ -447,7 +488,8 @@ class PerformanceNetFunction(torch.autograd.Function):
             for h in hooks:
                 h.ready(params)
         sink = module._grad_sink(on_ready if hooks else None)
-        g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need)
+        g_m, g_a, g_c = network_bwd(P, ctx.state, dy.contiguous(), sink, need,
+                                    aux=module._enc_stream())
         # the side stream's join event (None when the weight gradients ran on the compute
         # stream): an Event, so no hook closure of this backward outlives it
         module.__dict__["_mst_wgrad_joined"] = sink.joined

@@ -56,6 +56,9 @@ def slot_view(buf, p):
 _WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "1") == "1"
 # the last N backward blocks' weight gradients on the main stream (engine.GradSink); A/B knob
 _WGRAD_MAIN_TAIL = int(os.environ.get("MST_WGRAD_MAIN_TAIL", "2"))
+# the audio encoder on a second stream beside the MIDI / onset encoders (engine.network_fwd /
+# network_bwd); MST_ENC_STREAM=0 runs the encoders one after the other
+_ENC_STREAM = os.environ.get("MST_ENC_STREAM", "1") == "1"
 
 
 def set_wgrad_stream(on):
@@ -420,6 +423,16 @@ class PerformanceNet(nn.Module):
                 side = self.__dict__["_mst_side"] = torch.cuda.Stream(device=dev)
         return E.GradSink(flat_grad_of, on_ready, side, _WGRAD_MAIN_TAIL,
                           self.__dict__.get("_mst_bwd_blocks"))
+
+    def _enc_stream(self):
+        """The audio encoder's stream (None: serial; always under stream capture)."""
+        if not _ENC_STREAM or torch.cuda.is_current_stream_capturing():
+            return None
+        dev = torch.device("cuda", torch.cuda.current_device())
+        s = self.__dict__.get("_mst_enc")
+        if s is None or s.device != dev:
+            s = self.__dict__["_mst_enc"] = torch.cuda.Stream(device=dev)
+        return s
 
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
