@@ -369,6 +369,133 @@ __global__ __launch_bounds__(256, 2) void gemm_planes3_kernel(const PP p) {
     }
 }
 
+// ---- variant 4: v1's 128 x 256 tile and wave layout, BK = 16, FOUR 36 KB stages with two stages
+// of buffer_load ... lds in flight across each barrier (counted vmcnt: 36 pieces per stage, 5 for
+// waves 0-3 and 4 for waves 4-7). Question: is v1 bound by the DMA latency its two stages expose?
+constexpr int P4A = 128 * B2K, P4B = 256 * B2K;  // bf16 elements per A / B plane tile
+constexpr int STAGE4 = 3 * P4A + 3 * P4B;        // 36 KB
+constexpr int NST4 = 4;
+
+__global__ __launch_bounds__(NT, 1) void gemm_planes4_kernel(const PP p) {
+  __shared__ __attribute__((aligned(16))) char lds[NST4 * STAGE4 * 2];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  const int t = xcd_order(blockIdx.x + nx * blockIdx.y, nx * ny);
+  const int GM = ny < 8 ? ny : 8, grp = t / (GM * nx), fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM, tg = t - grp * GM * nx;
+  const int m0 = (fm + tg % gm) * BM, n0 = (tg / gm) * BN;
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0,
+                                                      (int)((2 * p.sa + (long long)p.M * p.lda) * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0,
+                                                      (int)((2 * p.sb + (long long)p.N * p.ldb) * 2), 0x00020000);
+  // pieces j = wave + 8 i < 36: j < 12 A (plane j / 4, rows 32 (j % 4) ..), else B (plane
+  // (j - 12) / 8, rows 32 ((j - 12) % 8) ..); lane l: row r0 + l / 2, slot l % 2 = quad ^ swz
+  uint32_t voff[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int j = wave + 8 * i;
+    const bool a = j < 12;
+    const int jj = a ? j : j - 12;
+    const int plane = a ? jj >> 2 : jj >> 3;
+    const int r = (a ? jj & 3 : jj & 7) * 32 + (lane >> 1);
+    const int q = (lane & 1) ^ ((r >> 3) & 1);
+    const long long row = a ? (long long)(m0 + r) : (long long)(n0 + r);
+    const bool in = j < 36 && (a ? (m0 + r < p.M) : (n0 + r < p.N));
+    const long long e = plane * (a ? p.sa : p.sb) + row * (a ? p.lda : p.ldb) + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
+  }
+  const bool five = wave < 4;  // wave-uniform: this wave moves 5 pieces per stage, else 4
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+    const int soff = kt * B2K * 2;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int j = wave + 8 * i;
+      if (j >= 36) break;
+      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE4 * 2 + j * 1024);
+      if (j < 12) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+    }
+  };
+  // wait until at most `ahead` later stages of this wave's pieces are in flight
+  auto wait_ahead = [&](int ahead) __attribute__((always_inline)) {
+    if (five) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    } else {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+  };
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = (p.K + B2K - 1) / B2K;
+  for (int k = 0; k < 3 && k < nk; ++k) issue(k, k);
+  wait_ahead(nk - 1 < 2 ? nk - 1 : 2);
+  __builtin_amdgcn_s_barrier();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 3;
+    if (kt + 3 < nk) issue((kt + 3) & 3, kt + 3);  // the buffer read one iteration ago
+    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE4;
+    const __bf16* Bp = Ap + 3 * P4A;
+    const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+    Split3 b0, b1, a0, a1;
+    {
+      const __bf16* q0 = Bp + off2(rb0, h);
+      b0.h = *reinterpret_cast<const bf16x8*>(q0);
+      b0.m = *reinterpret_cast<const bf16x8*>(q0 + P4B);
+      b0.l = *reinterpret_cast<const bf16x8*>(q0 + 2 * P4B);
+      const __bf16* q1 = Bp + off2(rb0 + 32, h);
+      b1.h = *reinterpret_cast<const bf16x8*>(q1);
+      b1.m = *reinterpret_cast<const bf16x8*>(q1 + P4B);
+      b1.l = *reinterpret_cast<const bf16x8*>(q1 + 2 * P4B);
+      const __bf16* q2 = Ap + off2(ra0, h);
+      a0.h = *reinterpret_cast<const bf16x8*>(q2);
+      a0.m = *reinterpret_cast<const bf16x8*>(q2 + P4A);
+      a0.l = *reinterpret_cast<const bf16x8*>(q2 + 2 * P4A);
+    }
+    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+    {
+      const __bf16* q3 = Ap + off2(ra0 + 32, h);
+      a1.h = *reinterpret_cast<const bf16x8*>(q3);
+      a1.m = *reinterpret_cast<const bf16x8*>(q3 + P4A);
+      a1.l = *reinterpret_cast<const bf16x8*>(q3 + 2 * P4A);
+    }
+    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+    // stage kt + 1 must have landed; stages kt + 2, kt + 3 (if issued) stay in flight
+    const int issued_ahead = (nk - 1 - kt) < 3 ? (nk - 1 - kt) : 3;  // stages after kt issued
+    wait_ahead(issued_ahead - 1);
+    __builtin_amdgcn_s_barrier();
+  }
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl = 128 * g + wn * 64 + j * 32 + r32;
+        Cs[ml * BN + nl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int nl = tid & (BN - 1);
+  if (n0 + nl < p.N)
+    for (int ml = tid >> 8; ml < BM && m0 + ml < p.M; ml += 2) p.C[(long long)(m0 + ml) * p.ldc + n0 + nl] = Cs[ml * BN + nl];
+}
+
 // reference: C = sum_k (A0+A1+A2)(B0+B1+B2) in double (naive)
 __global__ void ref_kernel(const PP p, double* Cr) {
   const int m = blockIdx.y, n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -444,13 +571,15 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
     p.A = da, p.B = db, p.C = dc;
-   for (int var = 1; var <= 3; ++var) {
-    dim3 grid = var == 1 ? dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM)
+   for (int var = 1; var <= 4; ++var) {
+    if (var == 2 || var == 3) continue;  // measured in profiles/r05/gemm_planes_micro*.txt
+    dim3 grid = var == 1 || var == 4 ? dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM)
               : var == 2 ? dim3((s.N + B2N - 1) / B2N, (s.M + B2M - 1) / B2M)
                          : dim3((s.N + 127) / 128, (s.M + 127) / 128);
     auto launch = [&]() {
       if (var == 1) hipLaunchKernelGGL(gemm_planes_kernel, grid, dim3(NT), 0, 0, p);
       else if (var == 2) hipLaunchKernelGGL(gemm_planes2_kernel, grid, dim3(NT), 0, 0, p);
+      else if (var == 4) hipLaunchKernelGGL(gemm_planes4_kernel, grid, dim3(NT), 0, 0, p);
       else hipLaunchKernelGGL(gemm_planes3_kernel, grid, dim3(256), 0, 0, p);
     };
     CK(hipMemset(dc, 0, (size_t)s.M * s.N * 4));
