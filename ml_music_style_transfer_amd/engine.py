@@ -333,17 +333,31 @@ def network_fwd(P, x_midi, x_audio, cond, drop_p=0.0, seed=0, depth=5, seed_dev=
         sv_o.append(sv)
         if i > 0:
             conds.append(c)
+    skips, sv_dn, ev = [None] * 4, [None] * 4, [None] * 4
     if aux is not None:
-        main.wait_stream(aux)
+        main.wait_stream(aux)  # the audio encoder (recorded before the dense levels are queued)
         _record((xa, enc_a, sv_a), main)
+        # the skip levels' DenseConcats need only the encoders: they run on aux beside
+        # dense_concats.0 and the up-convolution chain, which waits for each level's event
+        aux.wait_stream(main)
+        _record(enc_m, aux)
+        with torch.cuda.stream(aux):
+            for i in range(4):
+                skips[i], sv_dn[i] = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
+                                               enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1), seed_dev)
+                ev[i] = torch.cuda.Event()
+                ev[i].record(aux)
+        _record((skips, sv_dn), main)
     x, sv_d0 = dense_fwd(*_pp(P, "dense_concats.0", DN), xm, xa, drop_p, seed, seed_dev)
-    sv_dn, sv_up = [], []
+    sv_up = []
     for i in range(4):
-        skip, svd = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
-                              enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1), seed_dev)
+        if aux is None:
+            skips[i], sv_dn[i] = dense_fwd(*_pp(P, f"dense_concats.{i + 1}", DN), enc_m[-(i + 2)],
+                                           enc_a[-(i + 2)], drop_p, seed + 2 * (i + 1), seed_dev)
+        else:
+            main.wait_event(ev[i])
         cd = conds[i - 1] if i < 2 else None
-        x, svu = upconv_fwd(*_pp(P, f"up_convs.{i}", UP), skip, x, cd)
-        sv_dn.append(svd)
+        x, svu = upconv_fwd(*_pp(P, f"up_convs.{i}", UP), skips[i], x, cd)
         sv_up.append(svu)
     W, b = P["lastconv.weight"], P["lastconv.bias"]
     B, _, T = x.shape
@@ -372,6 +386,7 @@ def backward_param_order(depth=5):
 
 
 def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False), aux=None):
+    main = torch.cuda.current_stream()
     depth = st["depth"]
     y = st["y"]
     dypre = K.lrelu_bwd(dy, y)
@@ -401,9 +416,20 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False), aux=Non
         sink.block_done()
         if i < 2:
             d_conds[(i - 1) % 2] = d_cd
-        d_midi, d_audio = dense_bwd(_pp(P, f"dense_concats.{i + 1}", DN), svd, sink, d_res_pre,
-                                    gated=True)
-        sink.block_done()
+        if aux is not None:
+            # the skip level's DenseConcat backward feeds only the encoders' backward: on aux,
+            # beside the up-convolution chain
+            aux.wait_stream(main)
+            _record((d_res_pre, svd), aux)
+            with torch.cuda.stream(aux):
+                d_midi, d_audio = dense_bwd(_pp(P, f"dense_concats.{i + 1}", DN), svd, sink,
+                                            d_res_pre, gated=True)
+                sink.block_done()
+            d_midi.record_stream(main)
+        else:
+            d_midi, d_audio = dense_bwd(_pp(P, f"dense_concats.{i + 1}", DN), svd, sink, d_res_pre,
+                                        gated=True)
+            sink.block_done()
         d_before_m[depth - 2 - i] = d_midi
         d_before_a[depth - 2 - i] = d_audio
     d_xm, d_xa = dense_bwd(_pp(P, "dense_concats.0", DN), sv_d0, sink, dx, gated=True)
@@ -439,7 +465,8 @@ def network_bwd(P, st, dy, sink, need_input_grads=(False, False, False), aux=Non
 
     # the two encoders' backward are independent: with an aux stream the audio encoder's runs on
     # it beside the MIDI encoder's (enqueued second, so blocks finish in the flat-buffer order)
-    main = torch.cuda.current_stream()
+    if aux is not None:
+        main.wait_stream(aux)  # the skip levels' DenseConcat backward (d_before_m)
     g_m = encoder_bwd("down_convs", st["sv_m"], d_before_m, d_xm)
     if aux is not None:
         aux.wait_stream(main)
