@@ -359,13 +359,15 @@ def main():
     log = []
     graph_on[0] = False
     from ml_music_style_transfer_amd import model as model_mod
-    wgrad_side = model_mod._WGRAD_STREAM
+    wgrad_side, enc_side = model_mod._WGRAD_STREAM, model_mod._ENC_STREAM
     model_mod.set_wgrad_stream(False)  # per-launch times need the GEMMs serialised
+    model_mod.set_enc_stream(False)
     K.gemm_timing(log)
     for _ in range(args.kernel_timing_steps):
         step()
     K.gemm_timing(None)
     model_mod.set_wgrad_stream(wgrad_side)
+    model_mod.set_enc_stream(enc_side)
     torch.cuda.synchronize()
     gemm_ms = sum(ev[0].elapsed_time(ev[1]) for ev in log)
     gemm_flops = sum(ev[2] for ev in log)

@@ -67,6 +67,13 @@ def set_wgrad_stream(on):
     _WGRAD_STREAM = bool(on)
 
 
+def set_enc_stream(on):
+    """Enable / disable the encoder stream (process-wide; bench.py's per-launch timing leg
+    serialises it with the weight-gradient stream)."""
+    global _ENC_STREAM
+    _ENC_STREAM = bool(on)
+
+
 def _require_cuda(*ts):
     for t in ts:
         if t is not None and not t.is_cuda:
