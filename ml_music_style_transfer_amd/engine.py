@@ -69,6 +69,7 @@ class GradSink:
         # side stream still holds a backlog, so both streams then carry weight gradients
         self.block = 0
         self._main_from = blocks - main_tail if (blocks is not None and main_tail > 0) else None
+        self.home = torch.cuda.current_stream() if side is not None else None  # backward's main stream
 
     def target(self, p):
         self._pending.append(p)
@@ -81,11 +82,24 @@ class GradSink:
         return p.grad, True
 
     def wgrad(self, launch, *reads):
-        """Run a weight-gradient launch (on the side stream when there is one)."""
-        if self.side is None or (self._main_from is not None and self.block >= self._main_from):
+        """Run a weight-gradient launch (on the side stream when there is one; the tail blocks'
+        on the backward's main stream, which is idle by then while the encoder stream still
+        runs the audio encoder's backward)."""
+        if self.side is None:
             launch()
             return
-        main = torch.cuda.current_stream()
+        cur = torch.cuda.current_stream()
+        if self._main_from is not None and self.block >= self._main_from:
+            if cur == self.home:
+                launch()
+                return
+            self.home.wait_stream(cur)
+            with torch.cuda.stream(self.home):
+                launch()
+            for t in reads:
+                t.record_stream(self.home)
+            return
+        main = cur
         self.side.wait_stream(main)
         with torch.cuda.stream(self.side):
             launch()
@@ -109,7 +123,10 @@ class GradSink:
                 # streams' gradient kernels, and the main stream never waits for the weight
                 # gradients inside backward (joining it here, as rounds 1-4 did, serialised the
                 # two streams at every block whenever a DP reducer or BackwardAdam was attached)
-                self.side.wait_stream(torch.cuda.current_stream())
+                cur = torch.cuda.current_stream()
+                self.side.wait_stream(cur)
+                if cur != self.home:  # tail weight gradients may sit on the home stream
+                    self.side.wait_stream(self.home)
                 with torch.cuda.stream(self.side):
                     self.on_ready(self._pending)
             else:
