@@ -227,8 +227,10 @@ def main():
                     help="N=1: replay forward + L1 + backward + Adam as one captured hipGraph "
                          "(graphs.GraphedTrainStep); the STFT front end stays eager")
     ap.add_argument("--adam-overlap", action="store_true",
-                    help="Adam per bucket inside backward on a side stream (train.BackwardAdam) "
-                         "instead of one launch in opt.step()")
+                    help="(the default since round 5) Adam per bucket inside backward on a side "
+                         "stream (train.BackwardAdam), as train.main runs it")
+    ap.add_argument("--adam-step", action="store_true",
+                    help="Adam as one launch in opt.step() instead (the pre-round-5 default)")
     ap.add_argument("--loss", default="l1", choices=["l1", "mss", "l1+mss"],
                     help="training loss: train.py:132's L1 (the headline), the README's multi-scale "
                          "spectral loss on audio rendered with the target's phase, or both")
@@ -268,10 +270,12 @@ def main():
     dp.broadcast_parameters(model)
     if world > 1 and not args.no_overlap:
         dp.enable_overlapped_allreduce(model)
-    # --adam-overlap: Adam runs bucket by bucket inside backward on a side stream (the full
-    # update, overlapped with the GEMMs; +1.2 % per step at N=1, but the GEMMs it overlaps run
-    # slower, which the roofline leg then reports). Default: one launch in opt.step().
-    opt = make_optimizer(model, lr=1e-3, overlap_backward=args.adam_overlap and not args.no_overlap)
+    # Adam runs bucket by bucket inside backward on its own stream (train.BackwardAdam, bitwise
+    # the one-launch update; train.main does the same): since round 5's stream changes it beats
+    # the one launch in opt.step() by 1.5-2.3 % per step (profiles/r05/ab_step_adam_overlap_final
+    # .jsonl). --adam-step restores the one launch (and the in-step Adam timing leg).
+    adam_overlap = not args.adam_step and not args.graph
+    opt = make_optimizer(model, lr=1e-3, overlap_backward=adam_overlap and not args.no_overlap)
     if os.environ.get("MST_BENCH_PREALLOC", "0") == "1":  # A/B: Adam moments allocated up front
         opt.prepare()
 
@@ -286,8 +290,8 @@ def main():
     comm_on = [True]  # off only for the exposed-communication leg after the timed region
     gstep = None
     if args.graph:
-        if world > 1 or args.adam_overlap or args.loss != "l1":
-            raise SystemExit("--graph: single GPU, no --adam-overlap")
+        if world > 1 or args.loss != "l1":
+            raise SystemExit("--graph: single GPU, L1 loss")
         from ml_music_style_transfer_amd.graphs import GraphedTrainStep
         gstep = GraphedTrainStep(model, opt, warmup=1)
 
@@ -335,7 +339,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    adam_on[0] = gstep is None and not args.adam_overlap
+    adam_on[0] = gstep is None and not adam_overlap
     for _ in range(args.steps):
         loss = step()
     adam_on[0] = False
@@ -362,12 +366,17 @@ def main():
     wgrad_side, enc_side = model_mod._WGRAD_STREAM, model_mod._ENC_STREAM
     model_mod.set_wgrad_stream(False)  # per-launch times need the GEMMs serialised
     model_mod.set_enc_stream(False)
+    bwd_adam = getattr(opt, "_bwd", None)
+    if bwd_adam is not None:
+        bwd_adam.paused = True  # no Adam stream beside the timed GEMMs either
     K.gemm_timing(log)
     for _ in range(args.kernel_timing_steps):
         step()
     K.gemm_timing(None)
     model_mod.set_wgrad_stream(wgrad_side)
     model_mod.set_enc_stream(enc_side)
+    if bwd_adam is not None:
+        bwd_adam.paused = False
     torch.cuda.synchronize()
     gemm_ms = sum(ev[0].elapsed_time(ev[1]) for ev in log)
     gemm_flops = sum(ev[2] for ev in log)
@@ -453,14 +462,32 @@ def main():
         },
         "final_loss": round(final_loss, 5),
     }
+    adam_note = "the optimizer step of the timed steps"
+    if not adam_ev and adam_overlap and opt._flat_groups and gstep is None:
+        # the timed steps ran Adam per bucket inside backward: time the same kernel over the whole
+        # flat buffer in isolation, after every measured leg above (one more update of the state)
+        pf, gf, _ = model.flat_buffers()
+        st = next(iter(opt._flat_groups.values()))
+        evs = []
+        for _ in range(4):
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record()
+            K.adam(pf, gf, st["m"], st["v"], 1e-3, 0.9, 0.999, 1e-8, 1.0)
+            e[1].record()
+            evs.append(e)
+        torch.cuda.synchronize()
+        adam_ev = evs[1:]
+        adam_note = ("measured in isolation after the timed region (the timed steps run it per "
+                     "bucket inside backward, train.BackwardAdam)")
     if adam_ev:
-        # the optimizer step of the timed steps (one adam_kernel over the flat buffer, 28 B per
-        # parameter: p, m, v read + written, g read), HIP events on its launch stream
+        # one adam_kernel over the flat buffer, 28 B per parameter: p, m, v read + written, g
+        # read; HIP events on its launch stream
         n_par = int(model.flat_buffers()[2])  # the flat buffer the kernel streams (the dead MBR
         # convolutions' weights are not in it)
         a_ms = sum(e0.elapsed_time(e1) for e0, e1 in adam_ev) / len(adam_ev)
         a_gbs = 28.0 * n_par / (a_ms * 1e-3) / 1e9
         out["adam"] = {"kernel": "adam_kernel (flat fp32 p/g/m/v, torch.optim.Adam arithmetic)",
+                       "timing": adam_note, "inside_backward": bool(adam_overlap),
                        "bound": "hbm", "params": n_par, "bytes_per_step": 28 * n_par,
                        "ms_per_step": round(a_ms, 3), "achieved": round(a_gbs, 1),
                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a_gbs / HBM_PEAK_GBS, 4)}

@@ -257,6 +257,7 @@ class BackwardAdam:
         self.updates = 0  # steps whose update ran inside backward
         self.joined = None  # event of the last finish(): completes with that step's updates
         self.max_blocks = int(os.environ.get("MST_BWD_ADAM_BLOCKS", "256"))  # A/B tuning knob
+        self.paused = False  # True: step() runs the one-launch update (bench.py's GEMM timing leg)
 
     def _eligible(self):
         m = self.model
@@ -276,7 +277,7 @@ class BackwardAdam:
 
     def begin(self):
         self.active = self.launched = False
-        if not self._eligible():
+        if self.paused or not self._eligible():
             return
         group = self.opt.param_groups[0]
         index = self.model._flat["index"]
@@ -484,7 +485,9 @@ def main(args, return_model=False):
         dp.broadcast_parameters(model)         # every rank starts from rank 0's weights
         dp.enable_overlapped_allreduce(model)  # bucket all-reduces inside backward
         model._seed += rank << 24              # per-rank dropout streams
-    optimizer = make_optimizer(model, lr=1e-3)
+    # the reference loop steps after every backward (train.py:131-141), so the update runs per
+    # bucket inside backward (BackwardAdam: bitwise the one-launch update, 1.5-2.3 % faster)
+    optimizer = make_optimizer(model, lr=1e-3, overlap_backward=True)
     model.zero_grad()
     optimizer.zero_grad()
     scheduler = torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, 'min')
