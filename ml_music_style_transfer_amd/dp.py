@@ -7,11 +7,18 @@ collectives over contiguous slices — no gradient copies, no per-parameter call
 over ranks matches one large-batch step: L1 is a mean, so averaging per-rank gradients of
 per-rank means equals the gradient of the global mean for equal per-rank batches.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
 DEFAULT_BUCKET_BYTES = 256 << 20  # 256 MB: big buckets suit xGMI point-to-point rings
-OVERLAP_BUCKET_BYTES = 128 << 20  # smaller when overlapped: the last bucket is the exposed one
+# smaller when overlapped: the last bucket is the exposed one (MST_BUCKET_MB: A/B knob)
+OVERLAP_BUCKET_BYTES = int(os.environ.get("MST_BUCKET_MB", "128")) << 20
+# backward Adam's own buckets when no DP reducer is attached (N = 1; with a reducer it shares the
+# reducer's): 64 MB ran the step 0.5 % faster than 128 MB, 32 and 256 MB in between
+# (profiles/r05/ab_step_bucket_mb.jsonl; MST_ADAM_BUCKET_MB: A/B knob)
+ADAM_BUCKET_BYTES = int(os.environ.get("MST_ADAM_BUCKET_MB", "64")) << 20
 
 
 def is_dist():

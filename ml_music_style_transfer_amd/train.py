@@ -83,7 +83,7 @@ class Adam(torch.optim.Optimizer):
         self._owner = model
         return self
 
-    def overlap_backward(self, model=None, bucket_bytes=dp.OVERLAP_BUCKET_BYTES):
+    def overlap_backward(self, model=None, bucket_bytes=dp.ADAM_BUCKET_BYTES):
         """Run this optimizer's update inside the model's backward pass, bucket by bucket
         (BackwardAdam). Only for loops that call step() after every backward (the reference's
         train loop, train.py:131-141): no gradient accumulation across backward passes, no
