@@ -55,7 +55,7 @@ def slot_view(buf, p):
 # would make per-launch times meaningless). Stream capture (graphs.py) always runs serially.
 _WGRAD_STREAM = os.environ.get("MST_WGRAD_STREAM", "1") == "1"
 # the last N backward blocks' weight gradients on the main stream (engine.GradSink); A/B knob
-_WGRAD_MAIN_TAIL = int(os.environ.get("MST_WGRAD_MAIN_TAIL", "4"))
+_WGRAD_MAIN_TAIL = int(os.environ.get("MST_WGRAD_MAIN_TAIL", "6"))
 # the audio encoder on a second stream beside the MIDI / onset encoders (engine.network_fwd /
 # network_bwd); MST_ENC_STREAM=0 runs the encoders one after the other
 _ENC_STREAM = os.environ.get("MST_ENC_STREAM", "1") == "1"
