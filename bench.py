@@ -443,6 +443,9 @@ def main():
                            "dense fp32 MFMA peak; achieved counts fp32 multiply-adds"),
             "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
+            "frac_basis": ("achieved / peak, peak = the instruction ceiling above (since round 5); "
+                           "rounds 1-4 reported frac against the fp32 MFMA peak, which is "
+                           "frac_of_fp32_mfma_peak here: compare across rounds on that field"),
             "fp32_mfma_peak": PEAK_FP32_MFMA,
             "frac_of_fp32_mfma_peak": round(achieved / PEAK_FP32_MFMA, 4),
             "fp32_mfma_peak_basis": ("what an fp32 user gets against the chip's fp32 MFMA rate "

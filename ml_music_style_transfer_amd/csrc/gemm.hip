@@ -23,7 +23,6 @@
 // shares the SIMD's f32 datapath with VALU (rocprofv3: SQ_VALU_MFMA_COEXEC_CYCLES = 0), so
 // every loader VALU instruction costs MFMA issue time: the per-element index work is kept
 // wave-uniform (scalar) wherever the mapping allows it.
-#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -211,10 +210,6 @@ struct GP {
   const __bf16* pB;
   long long psa, psb;  // plane strides (elements)
   int pld;             // row stride = padded K (a multiple of BK)
-  // split-K fixup in the GEMM (splitk_epilogue): arrival counters after the slabs, launch tag
-  unsigned long long* cnt;
-  unsigned long long tag;
-  int fixup;
   int slab4;  // split-K slabs stored as dwordx4 rows (N % 4 == 0, M N < 2^29; store_slab4)
 };
 
@@ -679,19 +674,6 @@ constexpr int STAGE_BF = 3 * PLANE + 3 * PLANE_BW;  // bf16 elements per stage (
 constexpr int LDS_W_FLOATS = STAGE_BF;            // two stages = 144 KB; the 128 KB epilogue tile aliases
 static_assert(BM * BNW <= LDS_W_FLOATS, "epilogue tile must fit the two stages");
 
-// Split-K without a reduce launch (round 5). Every split of a 128 x 256 tile stores its partial
-// tile as a slab with write-through (sc1) dwordx4 stores; after every wave's vmcnt(0) wait and a
-// barrier, one lane adds the workgroup's arrival to the tile's counter (agent-scope atomic), and
-// the workgroup whose arrival completes the tile (told by the value its atomic returned) sums the
-// S slabs IN SPLIT ORDER with sc1 loads (bitwise the sum splitk_reduce4_kernel forms) and runs the
-// layer's epilogue: the hand-off is the first validated row of MI355X_MICROARCH.md's
-// inter-workgroup table (one workgroup per CU, sc1 stores and loads, counter add after the
-// waits). No workgroup ever waits for another. Counters are 64-bit words after the slabs,
-// (launch tag << 16) | arrivals: a word carrying another launch's tag counts as zero, so the
-// workspace needs no clearing (the stream arena and graph pools hand out dirty memory); the
-// last arrival clears its word, since graph replays reuse a launch's tag.
-constexpr int SC1 = 16;  // buffer instruction cache policy: sc1 (write-through / L2-bypassing read)
-
 // Split-K slab of a 128 x 256 tile from the LDS tile: one dwordx4 per thread per row, 16 row
 // passes with 32-bit offsets (the per-element stores did 64-bit index math for every element:
 // the weight-gradient kernels' short-K splits spent more VALU in that epilogue than in their
@@ -710,79 +692,6 @@ __device__ __forceinline__ void store_slab4(const GP& p, const float* Cs, int m0
     const f32x4 v = *reinterpret_cast<const f32x4*>(Cs + ml * BNW + 4 * q);
     const uint32_t vo = (ml < nrow && n < p.N) ? (uint32_t)((m0 + ml) * p.N + n) * 4u : OOB;
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)vo, 0, 0);
-  }
-}
-
-template <bool WG>
-__device__ __forceinline__ void splitk_epilogue(const GP& p, const float* Cs, int m0, int n0, int split,
-                                                int tile, int tid) {
-  constexpr int Q = BNW / 4;         // 64 float4 per tile row: one wave per row
-  constexpr int RPP = NTHRW / Q;     // 8 rows per pass
-  __shared__ int s_last;
-  const long long MN = (long long)p.M * p.N;  // < 2^29 (host), N % 32 == 0
-  const int q = tid & (Q - 1), r0 = tid / Q;
-  const int n = n0 + 4 * q;
-  const bool nin = n < p.N;  // a quad lies wholly inside or outside the matrix
-  {
-    const rsrc_t rs = mk_rsrc(p.ws + split * MN, MN);
-    for (int ml = r0; ml < BM && m0 + ml < p.M; ml += RPP) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(Cs + ml * BNW + 4 * q);
-      const uint32_t vo = nin ? (uint32_t)(((long long)(m0 + ml) * p.N + n) * 4) : OOB;
-      __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)vo, 0, SC1);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    unsigned long long* c = p.cnt + tile;
-    unsigned long long old = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), nw;
-    do {
-      nw = (old & ~0xFFFFull) == p.tag ? old + 1 : (p.tag | 1ull);
-    } while (!__hip_atomic_compare_exchange_strong(c, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT));
-    const int last = (int)(nw & 0xFFFFull) == p.splitk;
-    if (last) __hip_atomic_store(c, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last || !nin) return;
-  // the tile's last split: its 16 rows per thread summed slab by slab in split order, one batch
-  // of 16 dwordx4 loads in flight per slab
-  constexpr int RW = BM / RPP;
-  f32x4 v[RW];
-  const int nrow = p.M - m0 < BM ? p.M - m0 : BM;
-#pragma unroll
-  for (int i = 0; i < RW; ++i) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int s2 = 0; s2 < p.splitk; ++s2) {
-    f32x4 w[RW];
-    if (s2 == split) {
-#pragma unroll
-      for (int i = 0; i < RW; ++i) w[i] = *reinterpret_cast<const f32x4*>(Cs + (r0 + RPP * i) * BNW + 4 * q);
-    } else {
-      const rsrc_t rs = mk_rsrc(p.ws + s2 * MN, MN);
-#pragma unroll
-      for (int i = 0; i < RW; ++i) {
-        const int ml = r0 + RPP * i;
-        const uint32_t vo = ml < nrow ? (uint32_t)(((long long)(m0 + ml) * p.N + n) * 4) : OOB;
-        w[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, SC1));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < RW; ++i) v[i] = s2 == 0 ? w[i] : v[i] + w[i];
-  }
-#pragma unroll
-  for (int i = 0; i < RW; ++i) {
-    const int ml = r0 + RPP * i;
-    if (ml >= nrow) break;
-    const int m = m0 + ml;
-    if constexpr (WG) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wgrad_store(p, m, n + e, v[i][e]);
-    } else {
-      const float bm = p.bias ? p.bias[m] : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) conv_store_b(p, m, n + e, v[i][e], bm);
-    }
   }
 }
 
@@ -964,10 +873,6 @@ __device__ __forceinline__ void tile_pass_w(const GP& p, float* lds, int m_t, in
         Cs[ml * BNW + nl2] = acc[i][j][r];
       }
   __syncthreads();
-  if (p.fixup) {
-    splitk_epilogue<false>(p, Cs, m_t * BM, n_t * BNW, split, m_t * ((p.N + BNW - 1) / BNW) + n_t, tid);
-    return;
-  }
   if (p.slab4) {
     store_slab4(p, Cs, m_t * BM, n_t * BNW, split, tid);
     return;
@@ -989,11 +894,9 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_w_kernel(const GP p) {
   const int nx = (p.N + BNW - 1) / BNW, ny = (p.M + BM - 1) / BM;
   const int W = nx * ny * (int)gridDim.z;
   const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
-  // with the in-kernel fixup a tile's splits are dispatched together (split fastest), so its
-  // last arrival's slab sum overlaps other tiles' MFMA work instead of forming a tail
-  const int split = p.fixup ? t % p.splitk : t / (nx * ny);
+  const int split = t / (nx * ny);
   int m_t, n_t;
-  tile_of(p.fixup ? t / p.splitk : t - split * nx * ny, nx, ny, m_t, n_t);
+  tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
   const int kt0 = (int)((long long)split * p.nk / p.splitk);
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
   tile_pass_w<TAPS, AMODE, DUAL>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
@@ -1188,6 +1091,32 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
 
 constexpr int STAGE_P = STAGE_BF;  // 72 KB of bf16 per stage: A 3 x [128][32], B 3 x [256][32]
 
+// LDS-DMA piece (buffer_load_dwordx4 ... lds) as inline asm. As a builtin, hipcc inserts
+// s_waitcnt vmcnt(0) before the first ds_read after it (the DMA may alias the read), i.e. every K
+// tile waited for the NEXT stage's pieces before reading the current one. The asm is invisible to
+// that pass; the loop waits for its own pieces (vmcnt(0), then the barrier) before the stage is
+// read. M0 is saved and restored inside the statement (as fft.hip's dma_b128).
+__device__ __forceinline__ void dma_piece(rsrc_t rs, unsigned lds_addr, uint32_t voff, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
+
+// Round 6 (tools/micro/gemm_planes.hip, profiles/r06/gemm_planes_micro_stagger.txt): the asm DMA,
+// plus two measures for the two waves that share each SIMD (waves w and w + 4 run the same loop
+// in lockstep, reaching their fragment reads and the barrier together; MI355X_MICROARCH.md, "two
+// waves per SIMD", items 4 and 9):
+//  - a STAGGER: waves 4-7 run each K tile's second 16-deep half one barrier late, from fragments
+//    read into registers before the barrier (48 VGPRs), so after every barrier one wave per SIMD
+//    has MFMAs to issue at once while its partner reads its first fragments;
+//  - static priority s_setprio 1 for waves 4-7 (the arbitration losers otherwise).
+// The same products are summed in the same order per accumulator, so results are bitwise those of
+// the unstaggered loop. Micro: +2-5 % over the builtin-DMA loop on the step's wgrad / conv shapes
+// (e.g. 188.6 -> 195.7 TF/s on the L0 audio weight gradient, 172.7 -> 178.9 on L1).
 template <bool WG>
 __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int n_t, int kt0,
                                             int kt1, int split, int tid) {
@@ -1215,19 +1144,21 @@ __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int
     const long long e = plane * (a ? p.psa : p.psb) + (long long)row * p.pld + 8 * q;
     voff[i] = in ? (uint32_t)(e * 2) : OOB;
   }
+  const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address (low half of the flat one)
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
     const int soff = kt * BK * 2;
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
       const int j = wave + 8 * i;  // wave-uniform: A or B by a scalar branch
-      auto* dst = (__attribute__((address_space(3))) void*)(lds + (stage * STAGE_P) * 2 + j * 1024);
-      if (j < 24) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
-      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (stage * STAGE_P) * 2 + j * 1024);
+      if (j < 24) dma_piece(rA, dst, voff[i], soff);
+      else dma_piece(rB, dst, voff[i], soff);
     }
   };
   const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
   const int wm = (wave >> 1) & 1, wn = wave & 1;
   const int r32 = lane & 31, h = lane >> 5;
+  const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
   f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -1235,32 +1166,64 @@ __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto half = [&](const Split3& a0, const Split3& a1, const Split3& b0, const Split3& b1)
+      __attribute__((always_inline)) {
+    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+  };
+  const bool late = wave >= 4;  // the second wave on each SIMD
+  if (late) __builtin_amdgcn_s_setprio(1);
   if (kt0 < kt1) {
     issue(0, kt0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int st = (kt - kt0) & 1;
-      if (kt + 1 < kt1) issue(st ^ 1, kt + 1);
-      const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE_P;
-      const __bf16* Bp = Ap + 3 * PLANE;
-      const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+    if (!late) {
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const int st = (kt - kt0) & 1;
+        if (kt + 1 < kt1) issue(st ^ 1, kt + 1);
+        const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE_P;
+        const __bf16* Bp = Ap + 3 * PLANE;
 #pragma unroll
-      for (int s2 = 0; s2 < BK / 16; ++s2) {
-        const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, 2 * s2 + h);
-        const Split3 b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 * s2 + h);
-        const Split3 a0 = ld_planes<PLANE>(Ap, ra0, 2 * s2 + h);
-        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
-        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
-        const Split3 a1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 * s2 + h);
-        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
-        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+        for (int s2 = 0; s2 < BK / 16; ++s2) {
+          const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, 2 * s2 + h);
+          const Split3 b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 * s2 + h);
+          const Split3 a0 = ld_planes<PLANE>(Ap, ra0, 2 * s2 + h);
+          acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+          acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+          const Split3 a1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 * s2 + h);
+          acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+          acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+        }
+        // the next stage's DMA has landed and every wave is done reading this one
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
-      // the next stage's DMA has landed and every wave is done reading this one
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+    } else {
+      Split3 pa0, pa1, pb0, pb1;  // the previous K tile's second half, read before the barrier
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const int st = (kt - kt0) & 1;
+        if (kt + 1 < kt1) issue(st ^ 1, kt + 1);
+        if (kt > kt0) half(pa0, pa1, pb0, pb1);
+        const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE_P;
+        const __bf16* Bp = Ap + 3 * PLANE;
+        {
+          const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, h), b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, h);
+          const Split3 a0 = ld_planes<PLANE>(Ap, ra0, h), a1 = ld_planes<PLANE>(Ap, ra0 + 32, h);
+          half(a0, a1, b0, b1);
+        }
+        pb0 = ld_planes<PLANE_BW>(Bp, rb0, 2 + h);
+        pb1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 + h);
+        pa0 = ld_planes<PLANE>(Ap, ra0, 2 + h);
+        pa1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 + h);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      half(pa0, pa1, pb0, pb1);
     }
   }
+  if (late) __builtin_amdgcn_s_setprio(0);
   // epilogue: accumulators -> LDS tile (128 x 256 floats, aliasing the stages) -> rows
   float* Cs = reinterpret_cast<float*>(lds);
 #pragma unroll
@@ -1274,10 +1237,6 @@ __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int
         Cs[ml * BNW + nl] = acc[i][j][r];
       }
   __syncthreads();
-  if (p.fixup) {
-    splitk_epilogue<WG>(p, Cs, m0, n0, split, m_t * ((p.N + BNW - 1) / BNW) + n_t, tid);
-    return;
-  }
   if (p.slab4) {
     store_slab4(p, Cs, m0, n0, split, tid);
     return;
@@ -1302,11 +1261,9 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_p_kernel(const GP p) {
   const int nx = (p.N + BNW - 1) / BNW, ny = (p.M + BM - 1) / BM;
   const int W = nx * ny * (int)gridDim.z;
   const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
-  // with the in-kernel fixup a tile's splits are dispatched together (split fastest), so its
-  // last arrival's slab sum overlaps other tiles' MFMA work instead of forming a tail
-  const int split = p.fixup ? t % p.splitk : t / (nx * ny);
+  const int split = t / (nx * ny);
   int m_t, n_t;
-  tile_of(p.fixup ? t / p.splitk : t - split * nx * ny, nx, ny, m_t, n_t);
+  tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
   const int kt0 = (int)((long long)split * p.nk / p.splitk);
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
   tile_pass_p<WG>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
@@ -1584,30 +1541,6 @@ void choose_sched(GP& p, int req) {
   }
 }
 
-// Split-K reduced inside the 128 x 256 kernels (splitk_epilogue) instead of by a reduce launch:
-// opt-in, MST_SPLITK_FIXUP=1. Measured SLOWER in the training step: 38.0-38.4 vs 36.5-36.7
-// ms/step in two same-box alternations (profiles/r05/ab_step_splitk_fixup.jsonl; split-major and
-// tile-major dispatch alike): the split-K launches are sized to about one residency wave, so a
-// tile's slab sum runs on one CU while S - 1 of every S CUs idle, where the reduce launch spreads
-// the same bytes over the whole chip (the 1 x 1 dual-destination convs +27 % per launch, the
-// reduce launches' 2.5 ms/step of kernel time notwithstanding). Needs N % 32 == 0: slab rows are whole
-// 128-byte lines, so no cache line holds parts of two tiles (a last arrival's sc1 read would
-// otherwise leave a line in its XCD's L2 that another tile's producer then rewrites in memory,
-// and a later last arrival of that tile on the same XCD would read the stale copy); and slabs
-// addressable with 32-bit byte offsets.
-static int splitk_fixup_env() {
-  static const int v = [] {
-    const char* e = getenv("MST_SPLITK_FIXUP");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v;
-}
-
-bool fixup_ok(int M, int N, int splitk) {
-  return splitk_fixup_env() && splitk > 1 && splitk < 0xFFFF && N % 32 == 0 &&
-         (long long)M * N < (1ll << 29);
-}
-
 bool slab4_ok(int M, int N, int splitk) {  // MST_SLAB4=0: per-element slab stores (A/B)
   static const int env = [] {
     const char* e = getenv("MST_SLAB4");
@@ -1616,30 +1549,13 @@ bool slab4_ok(int M, int N, int splitk) {  // MST_SLAB4=0: per-element slab stor
   return env && splitk > 1 && N % 4 == 0 && (long long)M * N < (1ll << 29);
 }
 
-size_t fixup_cnt_bytes(int M, int N) {  // one 64-bit arrival counter per 128 x 256 tile
-  return (size_t)ceil_div(M, BM) * ceil_div(N, BNW) * sizeof(unsigned long long);
-}
-
-size_t round8(size_t x) { return (x + 7) / 8 * 8; }
-
-unsigned long long next_fixup_tag() {  // 48-bit launch tags, never 0
-  static std::atomic<unsigned long long> t{0};
-  unsigned long long v;
-  do v = (t.fetch_add(1) + 1) & 0xFFFFFFFFFFFFull;
-  while (v == 0);
-  return v << 16;
-}
-
-bool wide_fixup(const GP& p) { return p.wide && p.sk_L == 0 && fixup_ok(p.M, p.N, p.splitk); }
-
 size_t sched_ws_bytes(const GP& p) {
   if (p.sk_L > 0) {  // two partial-tile slots per workgroup of the launched grid
     const long long G = (p.sk_I + p.sk_L - 1) / p.sk_L;
     return p.sk_L % p.nk ? (size_t)(2 * G) * BM * BN * sizeof(float) : 0;
   }
   if (p.splitk <= 1) return 0;
-  const size_t slabs = (size_t)p.splitk * p.M * p.N * sizeof(float);
-  return wide_fixup(p) ? round8(slabs) + fixup_cnt_bytes(p.M, p.N) : slabs;
+  return (size_t)p.splitk * p.M * p.N * sizeof(float);
 }
 
 // Falls back to a single K pass (data-parallel) when the caller's workspace is too small.
@@ -1650,14 +1566,7 @@ void bind_ws(GP& p, float* ws, size_t ws_bytes) {
     p.splitk = 1;
   }
   p.ws = ws;
-  p.fixup = 0;
   p.slab4 = p.wide && p.sk_L == 0 && slab4_ok(p.M, p.N, p.splitk);
-  if (wide_fixup(p)) {
-    p.fixup = 1;
-    p.cnt = reinterpret_cast<unsigned long long*>(
-        reinterpret_cast<char*>(ws) + round8((size_t)p.splitk * p.M * p.N * sizeof(float)));
-    p.tag = next_fixup_tag();
-  }
 }
 
 template <bool WG>
@@ -1704,7 +1613,7 @@ int launch(const GP& p, hipStream_t st, int taps) {
     hipLaunchKernelGGL((sk_fixup_kernel<WG>), fg, dim3(256), 0, st, p);
     MST_CHECK_LAUNCH();
   }
-  if (p.splitk > 1 && !p.fixup) {
+  if (p.splitk > 1) {
     launch_reduce<WG>(p, st);
     MST_CHECK_LAUNCH();
   }
@@ -1885,7 +1794,7 @@ int build_wgrad(const mst_wgrad_desc* d, const mst_src& src, float* out, GP& p) 
 struct PlanesWG {
   GP p;
   PackArgs pa, pb;
-  size_t slab_bytes, a_bytes, b_bytes, cnt_bytes;
+  size_t slab_bytes, a_bytes, b_bytes;
 };
 
 static size_t round256(size_t x) { return (x + 255) / 256 * 256; }
@@ -1974,9 +1883,7 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
   w.slab_bytes = p.splitk > 1 ? round256((size_t)p.splitk * p.M * p.N * sizeof(float)) : 0;
   w.a_bytes = round256((size_t)(3 * p.psa) * 2);
   w.b_bytes = round256((size_t)(3 * p.psb) * 2);
-  p.fixup = fixup_ok(p.M, p.N, p.splitk) ? 1 : 0;
   p.slab4 = slab4_ok(p.M, p.N, p.splitk) ? 1 : 0;
-  w.cnt_bytes = p.fixup ? round256(fixup_cnt_bytes(p.M, p.N)) : 0;
   return MST_OK;
 }
 
@@ -1997,10 +1904,6 @@ int run_wgrad_planes(PlanesWG& w, float* ws, hipStream_t st) {
   w.pb.out = reinterpret_cast<__bf16*>(base + w.slab_bytes + w.a_bytes);
   p.pA = w.pa.out;
   p.pB = w.pb.out;
-  if (p.fixup) {
-    p.cnt = reinterpret_cast<unsigned long long*>(base + w.slab_bytes + w.a_bytes + w.b_bytes);
-    p.tag = next_fixup_tag();
-  }
   int rc = launch_pack(w.pa, st);
   if (rc) return rc;
   rc = launch_pack(w.pb, st);
@@ -2008,7 +1911,7 @@ int run_wgrad_planes(PlanesWG& w, float* ws, hipStream_t st) {
   dim3 grid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk);
   hipLaunchKernelGGL((gemm_p_kernel<true>), grid, dim3(NTHRW), 0, st, p);
   MST_CHECK_LAUNCH();
-  if (p.splitk > 1 && !p.fixup) {
+  if (p.splitk > 1) {
     launch_reduce<true>(p, st);
     MST_CHECK_LAUNCH();
   }
@@ -2056,7 +1959,7 @@ size_t mst_wgrad_workspace_size(const mst_wgrad_desc* d) {
   float* outs[2];
   if (!d) return 0;
   PlanesWG w;
-  if (use_wgrad_planes(d, w)) return w.slab_bytes + w.a_bytes + w.b_bytes + w.cnt_bytes;
+  if (use_wgrad_planes(d, w)) return w.slab_bytes + w.a_bytes + w.b_bytes;
   const int ns = wgrad_sources(d, srcs, outs);
   if (ns < 1) return 0;
   size_t need = 0;
@@ -2075,7 +1978,7 @@ int mst_conv_wgrad_f32(const mst_wgrad_desc* d, float* ws, size_t ws_bytes, void
   if (!d) return MST_EINVAL;
   {
     PlanesWG w;
-    if (use_wgrad_planes(d, w) && ws && ws_bytes >= w.slab_bytes + w.a_bytes + w.b_bytes + w.cnt_bytes &&
+    if (use_wgrad_planes(d, w) && ws && ws_bytes >= w.slab_bytes + w.a_bytes + w.b_bytes &&
         ((uintptr_t)ws & 255) == 0)
       return run_wgrad_planes(w, ws, (hipStream_t)stream);
   }

@@ -600,7 +600,9 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
                                int32_t T, float slope, const float* d_a, const float* d_pool0,
                                const float* d_pool1, float* dy, float* rowsum, void* stream) {
   MST_REQUIRE(y && mean && rstd && dy && rows > 0 && T > 1);
-  MST_REQUIRE(rows * (long long)T < (1ll << 29));  // 32-bit buffer byte offsets in in_bwd_kernel
+  // in_bwd_kernel addresses through 32-bit buffer byte offsets; larger tensors take the long-row
+  // kernel (64-bit addressing), as in the forward
+  const bool buf32 = rows * (long long)T < (1ll << 29);
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   int np = (T + 127) / 128;
@@ -612,15 +614,15 @@ int mst_instnorm_lrelu_bwd_f32(const float* y, const float* mean, const float* r
     if (even) hipLaunchKernelGGL((in_bwd_kernel<NP_, G_, true>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum); \
     else hipLaunchKernelGGL((in_bwd_kernel<NP_, G_, false>), GR, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum); \
   } while (0)
-  if (np <= 1 && g < 64) {
+  if (buf32 && np <= 1 && g < 64) {
     if (g == 4) MST_IN(1, 4, gs);
     else if (g == 8) MST_IN(1, 8, gs);
     else if (g == 16) MST_IN(1, 16, gs);
     else MST_IN(1, 32, gs);
-  } else if (np <= 1) MST_IN(1, 64, grid);
-  else if (np <= 2) MST_IN(2, 64, grid);
-  else if (np <= 4) MST_IN(4, 64, grid);
-  else if (np <= 8) MST_IN(8, 64, grid);
+  } else if (buf32 && np <= 1) MST_IN(1, 64, grid);
+  else if (buf32 && np <= 2) MST_IN(2, 64, grid);
+  else if (buf32 && np <= 4) MST_IN(4, 64, grid);
+  else if (buf32 && np <= 8) MST_IN(8, 64, grid);
 #undef MST_IN
   else hipLaunchKernelGGL(in_bwd_long_kernel, grid, block, 0, st, y, mean, rstd, rows, T, slope, d_a, d_pool0, d_pool1, dy, rowsum);
   MST_CHECK_LAUNCH();

@@ -74,12 +74,21 @@ def Process_Data(data_dir, n_train_read=None, n_test_read=None, batch_size=16, d
 class DeviceLoader:
     """DataLoader(dataset, batch_size, shuffle) over a Dataseth5py whose arrays live in HBM."""
 
-    def __init__(self, dataset, batch_size=16, shuffle=False, device="cuda", sampler=None):
+    def __init__(self, dataset, batch_size=16, shuffle=False, device="cuda", sampler=None,
+                 target_audio=None):
         self.dataset = dataset
         self.batch_size = batch_size
         self.shuffle = shuffle
         self.sampler = sampler  # e.g. torch DistributedSampler: one rank's shard per process
         self.device = torch.device(device)
+        # target_audio (optional): a map from a (b, 1025, T) batch of target spectrograms to its
+        # (b, L) waveforms (the multi-scale loss's Griffin-Lim target, train.make_loss). Each
+        # item's waveform is a constant of the item, so it is computed once, the first time the
+        # item is drawn, and kept in HBM; every batch's target then carries its rows as
+        # `target.mst_audio` (a device gather).
+        self.target_audio = target_audio
+        self._audio = None   # (styles, n, L) device buffer, allocated on first use
+        self._audio_done = None
         ds = dataset
         self.n = ds.n_data
         self.styles = list(ds.styles)
@@ -126,7 +135,29 @@ class DeviceLoader:
                 sty.append(self.styles.index(random.choice(self.styles)))
                 rnd.append(random.randint(0, self.n - 1))
             t = torch.tensor([idx, sty, rnd], dtype=torch.int64).to(self.device, non_blocking=True)
-            yield self.X[t[0]], self.S[t[1], t[2]], self.S[t[1], t[0]]
+            target = self.S[t[1], t[0]]
+            if self.target_audio is not None:
+                target.mst_audio = self._target_audio(idx, sty, t, target)
+            yield self.X[t[0]], self.S[t[1], t[2]], target
+
+    def _target_audio(self, idx, sty, t, target):
+        if self._audio_done is None:
+            self._audio_done = np.zeros((len(self.styles), self.n), dtype=bool)
+        miss = [j for j, (i, s) in enumerate(zip(idx, sty)) if not self._audio_done[s, i]]
+        # an item drawn twice in one batch is computed once
+        first = {}
+        for j in miss:
+            first.setdefault((sty[j], idx[j]), j)
+        if first:
+            rows = torch.tensor(sorted(first.values()), dtype=torch.int64, device=self.device)
+            wav = self.target_audio(target[rows])
+            if self._audio is None:
+                self._audio = torch.empty((len(self.styles), self.n, wav.shape[-1]),
+                                          dtype=wav.dtype, device=self.device)
+            self._audio[t[1][rows], t[0][rows]] = wav
+            for (s, i) in first:
+                self._audio_done[s, i] = True
+        return self._audio[t[1], t[0]]
 
 
 def write_split(path, pianoroll, onoff, specs):

@@ -66,12 +66,25 @@ class GradSink:
         self.joined = None
         # the weight gradients of the last `main_tail` blocks (of `blocks` in the previous
         # backward) run on the main stream: once the main stream's input gradients are done the
-        # side stream still holds a backlog, so both streams then carry weight gradients
+        # side stream still holds a backlog, so both streams then carry weight gradients. At
+        # least one block keeps its weight gradients on the side stream (so join() always has
+        # the side stream's last launch to wait for).
         self.block = 0
-        self._main_from = blocks - main_tail if (blocks is not None and main_tail > 0) else None
+        if blocks is not None and main_tail > 0 and blocks > 1:
+            self._main_from = blocks - min(main_tail, blocks - 1)
+        else:
+            self._main_from = None
         self.home = torch.cuda.current_stream() if side is not None else None  # backward's main stream
+        # streams that wrote gradients in this backward (the encoder stream writes some): with no
+        # side stream the listeners issue from whichever stream is current at a block boundary,
+        # so that stream first waits for the others (a bucket may span blocks of two streams)
+        self._writers = []
 
     def target(self, p):
+        if self.on_ready is not None and self.side is None:
+            cur = torch.cuda.current_stream()
+            if cur not in self._writers:
+                self._writers.append(cur)
         self._pending.append(p)
         if p.grad is None:
             g = self.flat_grad_of(p)
@@ -130,6 +143,13 @@ class GradSink:
                 with torch.cuda.stream(self.side):
                     self.on_ready(self._pending)
             else:
+                # a bucket completed here may hold gradients another stream wrote (the skip
+                # levels' DenseConcat backward on the encoder stream): the listeners' collectives
+                # and updates issue from the current stream, so it waits for those writers first
+                cur = torch.cuda.current_stream()
+                for s in self._writers:
+                    if s != cur:
+                        cur.wait_stream(s)
                 self.on_ready(self._pending)
         self._pending = []
         self.block += 1

@@ -361,25 +361,35 @@ def make_loss(name="l1", mss_phase="griffinlim", gl_iters=8, alpha=1.0, sizes=No
               the Griffin-Lim reconstruction of the target spectrogram (gl_iters iterations; the
               HDF5 data holds no audio), the prediction is rendered with mss_phase's phase
               ("griffinlim": its own reconstruction's, "target": the target reconstruction's);
-      l1+mss  their sum."""
+      l1+mss  their sum.
+    The target waveform is a constant of each item: a data.DeviceLoader given
+    `loss_fn.target_audio` as its target_audio computes it once per item and hands it over as
+    `target.mst_audio`; a target without it (any other loader) is reconstructed per call. Griffin-
+    Lim from the same spectrogram is bitwise the same per clip in any batch (spectral.griffinlim),
+    so both paths give the same loss."""
     if name not in LOSSES:
         raise ValueError(f"loss {name!r}: one of {LOSSES}")
     from . import spectral
 
+    def target_audio(target):
+        with torch.no_grad():
+            return spectral.griffinlim(target, n_iter=gl_iters, hop_length=hop, init=None,
+                                       from_logpow=True)
+
     def mss(y_pred, target):
         if y_pred.shape != target.shape:
             raise ValueError("the multi-scale loss needs T = 12 (mod 16) (model.py:229-232)")
-        with torch.no_grad():
-            y_t = spectral.griffinlim(target, n_iter=gl_iters, hop_length=hop, init=None,
-                                      from_logpow=True)
+        y_t = getattr(target, "mst_audio", None)
+        if y_t is None:
+            y_t = target_audio(target)
         return spectral.spectrogram_mss_loss(y_pred, y_t, phase=mss_phase, hop=hop, alpha=alpha,
                                              sizes=sizes, gl_iters=gl_iters)
 
     if name == "l1":
         return E.l1_loss
-    if name == "mss":
-        return mss
-    return lambda y_pred, target: E.l1_loss(y_pred, target) + mss(y_pred, target)
+    fn = mss if name == "mss" else (lambda y_pred, target: E.l1_loss(y_pred, target) + mss(y_pred, target))
+    fn.target_audio = target_audio
+    return fn
 
 
 def train(model, epoch, train_loader, optimizer, iter_train_loss, log_every=2, loss_fn=None):
@@ -507,6 +517,8 @@ def main(args, return_model=False):
                 tr, num_replicas=world, rank=rank, shuffle=True))
             test_loader = DeviceLoader(te, args.batch_size, sampler=DistributedSampler(
                 te, num_replicas=world, rank=rank, shuffle=False))
+        # the multi-scale loss's target waveform: once per item, kept in HBM beside the split
+        train_loader.target_audio = getattr(loss_fn, "target_audio", None)
     else:
         T = args.frames
         train_ds = SyntheticSpectrogramDataset(args.n_train_read or 32, T=T, seed=1)

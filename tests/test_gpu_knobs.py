@@ -21,7 +21,6 @@ KNOBS = [
     {"MST_GEMM_WIDE": "0"},         # conv / dgrad on the 128 x 128 kernel
     {"MST_GEMM_SCHED": "sk"},       # stream-K for every GEMM
     {"MST_SPLITK_TAU": "1e-9"},     # split-K cost model pushed to no split
-    {"MST_SPLITK_FIXUP": "1"},      # split-K slabs summed inside the GEMM by each tile's last split
     {"MST_SLAB4": "0"},             # split-K slabs stored element by element
     {"MST_REDUCE_ROWS": "0"},       # split-K reduce as a 1-D float4 grid (a division per element)
     {"MST_WG_PLANES": "0"},         # wgrad on the register-split 128 x 128 kernel (K classes)

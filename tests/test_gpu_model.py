@@ -250,33 +250,49 @@ def test_adam_inside_backward_matches_step(cuda):
 
 
 def test_wgrad_side_stream_bitwise(cuda):
-    """Weight-gradient GEMMs on the side stream (the default) produce bitwise the same
-    gradients as the serial order, at the training batch's time axis, with and without
-    backward Adam (which joins the side stream before each bucket update)."""
+    """Every concurrent stream layout of the training step produces bitwise the serial order's
+    gradients and parameters, at the training batch's time axis, over three steps per network
+    (from the second backward on, the weight-gradient tail of MST_WGRAD_MAIN_TAIL blocks runs on
+    the home stream, since GradSink takes the block count from the previous backward):
+    weight-gradient side stream on / off x encoder stream on / off, each without and with backward
+    Adam on small (8 MB) buckets. Backward Adam with the side stream off and the encoder stream
+    on is the layout where a bucket spanning a skip-level DenseConcat (written on the encoder
+    stream) and the next up-convolution block (main stream) must wait for both writers
+    (engine.GradSink.block_done)."""
     from ml_music_style_transfer_amd import engine as E
     from ml_music_style_transfer_amd import model as M
     from ml_music_style_transfer_amd.train import make_optimizer
     xm, xa, cd, tg = _inputs(2, 252, cuda)
-    keep = M._WGRAD_STREAM
+    keep = (M._WGRAD_STREAM, M._ENC_STREAM)
+    steps = 3
+
+    def run(side, enc, overlap):
+        M.set_wgrad_stream(side)
+        M.set_enc_stream(enc)
+        net = _det_model(cuda).eval()
+        opt = make_optimizer(net, lr=1e-3)
+        if overlap:
+            opt.overlap_backward(bucket_bytes=8 << 20)
+        for _ in range(steps):
+            opt.zero_grad()
+            E.l1_loss(net(xm, xa, cd), tg).backward()
+            g = net.flat_buffers()[1].clone()
+            opt.step()
+            yield g, net.flat_buffers()[0].clone()
+
     try:
         for overlap in (False, True):
-            res = []
-            for side in (False, True):
-                M.set_wgrad_stream(side)
-                net = _det_model(cuda).eval()
-                opt = make_optimizer(net, lr=1e-3)
-                if overlap:
-                    opt.overlap_backward(bucket_bytes=8 << 20)
-                opt.zero_grad()
-                E.l1_loss(net(xm, xa, cd), tg).backward()
-                _, g, _ = net.flat_buffers()
-                g = g.clone()
-                opt.step()
-                res.append((g, net.flat_buffers()[0].clone()))
-            assert torch.equal(res[0][0], res[1][0]), overlap
-            assert torch.equal(res[0][1], res[1][1]), overlap
+            ref = list(run(False, False, overlap))  # serial: one stream
+            for side, enc in ((True, False), (False, True), (True, True)):
+                for it, (g, p) in enumerate(run(side, enc, overlap)):
+                    assert torch.equal(ref[it][0], g), (overlap, side, enc, it, "grad")
+                    assert torch.equal(ref[it][1], p), (overlap, side, enc, it, "param")
+                    del g, p
+            del ref
+            torch.cuda.empty_cache()
     finally:
-        M.set_wgrad_stream(keep)
+        M.set_wgrad_stream(keep[0])
+        M.set_enc_stream(keep[1])
 
 
 def test_side_streams_joined_once_main_stream_synced(cuda):

@@ -215,6 +215,41 @@ def test_device_loader_reproduces_dataloader(tmp_path):
                 assert torch.equal(a, b)
 
 
+def test_device_loader_target_audio_once_per_item(tmp_path):
+    """DeviceLoader(target_audio=f): every batch's target carries f(target) row for row as
+    `target.mst_audio`, f runs once per (style, item) over all epochs (the multi-scale loss's
+    Griffin-Lim target is a constant of the item, train.make_loss), and the batches themselves are
+    unchanged (same draws as without it)."""
+    import torch
+    from ml_music_style_transfer_amd import data
+    pr, oo, specs = _split(np.random.default_rng(11), N=7)
+    path = str(tmp_path / "d_train.hdf5")
+    data.write_split(path, pr, oo, specs)
+    calls = []
+
+    def f(target):  # a stand-in for the Griffin-Lim reconstruction: any per-row map
+        calls.append(target.shape[0])
+        return target.sum(1) * 0.5 + target[:, 3]
+
+    import random
+    torch.manual_seed(2)
+    random.seed(2)
+    dl0 = data.DeviceLoader(data.Dataseth5py(path), batch_size=4, shuffle=True, device="cpu")
+    plain = [b for _ in range(3) for b in dl0]
+    torch.manual_seed(2)
+    random.seed(2)
+    dl = data.DeviceLoader(data.Dataseth5py(path), batch_size=4, shuffle=True, device="cpu",
+                           target_audio=f)
+    got = [b for _ in range(3) for b in dl]
+    assert len(got) == len(plain) == 6
+    for (x, c, y), (x0, c0, y0) in zip(got, plain):
+        assert torch.equal(x, x0) and torch.equal(c, c0) and torch.equal(y, y0)
+        assert torch.equal(y.mst_audio, f(y))
+    drawn = dl._audio_done.sum()
+    assert sum(calls[:-len(got)]) == drawn  # (the checks above called f once per batch too)
+    assert drawn <= len(dl.styles) * dl.n
+
+
 def test_musicnet_solo_piano_filter(tmp_path):
     """extract_piano_pieces_from_musicnet_dataset.py:10-24: keep label files whose only
     instrument is 1 (piano)."""

@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+#include <algorithm>
 
 #define CK(x)                                                                   \
   do {                                                                          \
@@ -73,8 +74,41 @@ __device__ __forceinline__ int xcd_order(int w, int W) {
   return xcd * q + min(xcd, r) + (w >> 3);
 }
 
+
+// LDS-DMA as inline asm: hipcc does not model it, so it does not insert the s_waitcnt vmcnt(0) it
+// puts before every ds_read that may alias a builtin LDS-DMA (which waits for the NEXT stage's
+// pieces before reading the current one, i.e. exposes the DMA latency on every K tile). M0 is
+// written and restored inside the statement; the kernel counts vmcnt itself.
+__device__ __forceinline__ void dma_asm(rsrc_t rs, unsigned lds_addr, uint32_t voff, int soff) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds_addr), "s"(soff)
+      : "memory");
+}
+template <int ASM>
+__device__ __forceinline__ void dma16(rsrc_t rs, char* lds, int byte_off, uint32_t voff, int soff) {
+  if constexpr (ASM) {
+    dma_asm(rs, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lds + byte_off), voff, soff);
+  } else {
+    auto* dst = (__attribute__((address_space(3))) void*)(lds + byte_off);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, dst, 16, voff, soff, 0, 0);
+  }
+}
+
+// MODE 0: builtin DMA (v1); 1: asm DMA (v5); 2: asm DMA spread over the MFMAs (v6)
+__device__ unsigned long long g_clk[4 * 65536];  // MODE 3: per workgroup memtime / realtime at start / end
+
+template <int MODE>
 __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(const PP p) {
   __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  const unsigned wg_lin = blockIdx.x + gridDim.x * blockIdx.y;
+  if (MODE == 3 && threadIdx.x == 0 && wg_lin < 65536) {
+    g_clk[4 * wg_lin] = __builtin_amdgcn_s_memtime();
+    g_clk[4 * wg_lin + 1] = __builtin_amdgcn_s_memrealtime();
+  }
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
@@ -107,15 +141,14 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(const PP p) {
     voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
     isA[i] = a;
   }
+  auto piece = [&](int i, int stage, int kt) __attribute__((always_inline)) {
+    const int j = wave + 8 * i;
+    if (j < 24) dma16<MODE != 0>(rA, lds, stage * STAGE * 2 + j * 1024, voff[i], kt * BK * 2);
+    else dma16<MODE != 0>(rB, lds, stage * STAGE * 2 + j * 1024, voff[i], kt * BK * 2);
+  };
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
-    const int soff = kt * BK * 2;  // k offset in bytes
 #pragma unroll
-    for (int i = 0; i < 9; ++i) {
-      const int j = wave + 8 * i;
-      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE * 2 + j * 1024);
-      if (isA[i]) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
-      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
-    }
+    for (int i = 0; i < 9; ++i) piece(i, stage, kt);
   };
   const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
   const int wm = (wave >> 1) & 1, wn = wave & 1;
@@ -133,17 +166,28 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(const PP p) {
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int st = kt & 1;
-    if (kt + 1 < nk) issue(st ^ 1, kt + 1);
+    const bool more = kt + 1 < nk;
+    if (MODE != 2 && more) issue(st ^ 1, kt + 1);  // MODE 3: as MODE 1
     const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE;
     const __bf16* Bp = Ap + 3 * PA;
     const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+    // MODE 2: the next stage's 9 pieces in four groups after the reads of each 12-MFMA group
 #pragma unroll
     for (int s = 0; s < BK / 16; ++s) {
       const Split3 b0 = ld_planes<PB>(Bp, rb0, 2 * s + h), b1 = ld_planes<PB>(Bp, rb0 + 32, 2 * s + h);
       const Split3 a0 = ld_planes<PA>(Ap, ra0, 2 * s + h);
+      if (MODE == 2 && more) {  // pieces 0, 1 (s = 0) / 5, 6 (s = 1)
+        piece(5 * s, st ^ 1, kt + 1);
+        piece(5 * s + 1, st ^ 1, kt + 1);
+      }
       acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
       acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
       const Split3 a1 = ld_planes<PA>(Ap, ra0 + 32, 2 * s + h);
+      if (MODE == 2 && more) {  // pieces 2, 3, 4 (s = 0) / 7, 8 (s = 1)
+        piece(5 * s + 2, st ^ 1, kt + 1);
+        piece(5 * s + 3, st ^ 1, kt + 1);
+        if (s == 0) piece(4, st ^ 1, kt + 1);
+      }
       acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
       acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
     }
@@ -166,6 +210,143 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes_kernel(const PP p) {
   const int nl = tid & (BN - 1);
   if (n0 + nl < p.N)
     for (int ml = tid >> 8; ml < BM && m0 + ml < p.M; ml += 2) p.C[(long long)(m0 + ml) * p.ldc + n0 + nl] = Cs[ml * BN + nl];
+  if (MODE == 3 && threadIdx.x == 0 && wg_lin < 65536) {
+    g_clk[4 * wg_lin + 2] = __builtin_amdgcn_s_memtime();
+    g_clk[4 * wg_lin + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+
+// ---- variants 8-12: v5 (asm DMA) plus: CLK in-kernel clock stamps (s_memtime / s_memrealtime per
+// workgroup); STAG a stagger (MI355X_MICROARCH.md "two waves per SIMD" item 9): waves 4-7 (the
+// second wave on each SIMD) run each K tile's second 16-deep half one barrier late, from fragments
+// read into registers before the barrier, so after every barrier one wave per SIMD issues MFMAs
+// at once while its partner reads its next fragments; PRIO s_setprio 1 for waves 4-7 (item 4).
+template <bool CLK, bool STAG, bool PRIO>
+__global__ __launch_bounds__(NT, 1) void gemm_planes_x_kernel(const PP p) {
+  __shared__ __attribute__((aligned(16))) char lds[LDS_BYTES];
+  const unsigned wg_lin = blockIdx.x + gridDim.x * blockIdx.y;
+  if (CLK && threadIdx.x == 0 && wg_lin < 65536) {
+    g_clk[4 * wg_lin] = __builtin_amdgcn_s_memtime();
+    g_clk[4 * wg_lin + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nx = (p.N + BN - 1) / BN, ny = (p.M + BM - 1) / BM;
+  const int t = xcd_order(blockIdx.x + nx * blockIdx.y, nx * ny);
+  const int GM = ny < 8 ? ny : 8, grp = t / (GM * nx), fm = grp * GM;
+  const int gm = ny - fm < GM ? ny - fm : GM, tg = t - grp * GM * nx;
+  const int m0 = (fm + tg % gm) * BM, n0 = (tg / gm) * BN;
+  const rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0,
+                                                      (int)((2 * p.sa + (long long)p.M * p.lda) * 2), 0x00020000);
+  const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0,
+                                                      (int)((2 * p.sb + (long long)p.N * p.ldb) * 2), 0x00020000);
+  uint32_t voff[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int j = wave + 8 * i;
+    const bool a = j < 24;
+    const int jj = a ? j : j - 24;
+    const int plane = a ? jj / 8 : jj / 16;
+    const int r = (a ? jj % 8 : jj % 16) * 16 + (lane >> 2);
+    const int q = (lane & 3) ^ pl_swz(r);
+    const long long row = a ? (long long)(m0 + r) : (long long)(n0 + r);
+    const bool in = a ? (m0 + r < p.M) : (n0 + r < p.N);
+    const long long e = plane * (a ? p.sa : p.sb) + row * (a ? p.lda : p.ldb) + 8 * q;
+    voff[i] = in ? (uint32_t)(e * 2) : 0x7FFFFFF0u;
+  }
+  auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int j = wave + 8 * i;
+      if (j < 24) dma16<1>(rA, lds, stage * STAGE * 2 + j * 1024, voff[i], kt * BK * 2);
+      else dma16<1>(rB, lds, stage * STAGE * 2 + j * 1024, voff[i], kt * BK * 2);
+    }
+  };
+  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);
+  const int wm = (wave >> 1) & 1, wn = wave & 1;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto half = [&](const Split3& a0, const Split3& a1, const Split3& b0, const Split3& b1)
+      __attribute__((always_inline)) {
+    acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+    acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+    acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+    acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+  };
+  const int nk = (p.K + BK - 1) / BK;
+  if (PRIO && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const bool late = STAG && wave >= 4;  // wave-uniform
+  if (!late) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const int st = kt & 1;
+      if (kt + 1 < nk) issue(st ^ 1, kt + 1);
+      const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE;
+      const __bf16* Bp = Ap + 3 * PA;
+#pragma unroll
+      for (int s = 0; s < BK / 16; ++s) {
+        const Split3 b0 = ld_planes<PB>(Bp, rb0, 2 * s + h), b1 = ld_planes<PB>(Bp, rb0 + 32, 2 * s + h);
+        const Split3 a0 = ld_planes<PA>(Ap, ra0, 2 * s + h);
+        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
+        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
+        const Split3 a1 = ld_planes<PA>(Ap, ra0 + 32, 2 * s + h);
+        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
+        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    Split3 pa0, pa1, pb0, pb1;  // the previous tile's second half, read before the barrier
+    for (int kt = 0; kt < nk; ++kt) {
+      const int st = kt & 1;
+      if (kt + 1 < nk) issue(st ^ 1, kt + 1);
+      if (kt > 0) half(pa0, pa1, pb0, pb1);
+      const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + st * STAGE;
+      const __bf16* Bp = Ap + 3 * PA;
+      {
+        const Split3 b0 = ld_planes<PB>(Bp, rb0, h), b1 = ld_planes<PB>(Bp, rb0 + 32, h);
+        const Split3 a0 = ld_planes<PA>(Ap, ra0, h), a1 = ld_planes<PA>(Ap, ra0 + 32, h);
+        half(a0, a1, b0, b1);
+      }
+      pb0 = ld_planes<PB>(Bp, rb0, 2 + h);
+      pb1 = ld_planes<PB>(Bp, rb0 + 32, 2 + h);
+      pa0 = ld_planes<PA>(Ap, ra0, 2 + h);
+      pa1 = ld_planes<PA>(Ap, ra0 + 32, 2 + h);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (nk > 0) half(pa0, pa1, pb0, pb1);
+  }
+  float* Cs = reinterpret_cast<float*>(lds);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int nl = 128 * g + wn * 64 + j * 32 + r32;
+        Cs[ml * BN + nl] = acc[i][j][r];
+      }
+  __syncthreads();
+  const int nl = tid & (BN - 1);
+  if (n0 + nl < p.N)
+    for (int ml = tid >> 8; ml < BM && m0 + ml < p.M; ml += 2) p.C[(long long)(m0 + ml) * p.ldc + n0 + nl] = Cs[ml * BN + nl];
+  if (CLK && threadIdx.x == 0 && wg_lin < 65536) {
+    g_clk[4 * wg_lin + 2] = __builtin_amdgcn_s_memtime();
+    g_clk[4 * wg_lin + 3] = __builtin_amdgcn_s_memrealtime();
+  }
 }
 
 // ---- variant 2: 256 x 256 tile, BK = 16, three LDS stages (48 KB each) with one stage of
@@ -376,6 +557,7 @@ constexpr int P4A = 128 * B2K, P4B = 256 * B2K;  // bf16 elements per A / B plan
 constexpr int STAGE4 = 3 * P4A + 3 * P4B;        // 36 KB
 constexpr int NST4 = 4;
 
+template <int ASM>  // 0: builtin DMA (v4); 1: asm DMA (v7)
 __global__ __launch_bounds__(NT, 1) void gemm_planes4_kernel(const PP p) {
   __shared__ __attribute__((aligned(16))) char lds[NST4 * STAGE4 * 2];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -412,9 +594,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_planes4_kernel(const PP p) {
     for (int i = 0; i < 5; ++i) {
       const int j = wave + 8 * i;
       if (j >= 36) break;
-      auto* dst = (__attribute__((address_space(3))) void*)(lds + stage * STAGE4 * 2 + j * 1024);
-      if (j < 12) __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, dst, 16, voff[i], soff, 0, 0);
-      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, dst, 16, voff[i], soff, 0, 0);
+      if (j < 12) dma16<ASM>(rA, lds, stage * STAGE4 * 2 + j * 1024, voff[i], soff);
+      else dma16<ASM>(rB, lds, stage * STAGE4 * 2 + j * 1024, voff[i], soff);
     }
   };
   // wait until at most `ahead` later stages of this wave's pieces are in flight
@@ -545,7 +726,8 @@ int main(int argc, char** argv) {
       {2048, 8064, 4608, "conv fwd L1 audio (M=Cout, N=B T, K=3 Cin)"},
       {1536, 8064, 4608, "conv fwd L0 audio"},
   };
-  const bool check = argc > 1;
+  const bool check = argc > 1 && atoi(argv[1]) != 0;
+  const int only = argc > 2 ? atoi(argv[2]) : 0;  // one variant
   for (const Shape& s : shapes) {
     const int Kp = (s.K + 31) / 32 * 32;
     PP p{};
@@ -571,16 +753,21 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(da, ha.data(), ha.size() * 2, hipMemcpyHostToDevice));
     CK(hipMemcpy(db, hb.data(), hb.size() * 2, hipMemcpyHostToDevice));
     p.A = da, p.B = db, p.C = dc;
-   for (int var = 1; var <= 4; ++var) {
-    if (var == 2 || var == 3) continue;  // measured in profiles/r05/gemm_planes_micro*.txt
-    dim3 grid = var == 1 || var == 4 ? dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM)
-              : var == 2 ? dim3((s.N + B2N - 1) / B2N, (s.M + B2M - 1) / B2M)
-                         : dim3((s.N + 127) / 128, (s.M + 127) / 128);
+   for (int var = 1; var <= 12; ++var) {
+    if (var == 2 || var == 3 || var == 4 || var == 6 || var == 7) continue;  // measured: profiles/r05/gemm_planes_micro*.txt, profiles/r06/
+    if (only && var != only) continue;
+    dim3 grid = dim3((s.N + BN - 1) / BN, (s.M + BM - 1) / BM);
     auto launch = [&]() {
-      if (var == 1) hipLaunchKernelGGL(gemm_planes_kernel, grid, dim3(NT), 0, 0, p);
-      else if (var == 2) hipLaunchKernelGGL(gemm_planes2_kernel, grid, dim3(NT), 0, 0, p);
-      else if (var == 4) hipLaunchKernelGGL(gemm_planes4_kernel, grid, dim3(NT), 0, 0, p);
-      else hipLaunchKernelGGL(gemm_planes3_kernel, grid, dim3(256), 0, 0, p);
+      if (var == 1) hipLaunchKernelGGL(gemm_planes_kernel<0>, grid, dim3(NT), 0, 0, p);
+      else if (var == 5) hipLaunchKernelGGL(gemm_planes_kernel<1>, grid, dim3(NT), 0, 0, p);
+      else if (var == 6) hipLaunchKernelGGL(gemm_planes_kernel<2>, grid, dim3(NT), 0, 0, p);
+      else if (var == 4) hipLaunchKernelGGL(gemm_planes4_kernel<0>, grid, dim3(NT), 0, 0, p);
+      else if (var == 7) hipLaunchKernelGGL(gemm_planes4_kernel<1>, grid, dim3(NT), 0, 0, p);
+      else if (var == 8) hipLaunchKernelGGL((gemm_planes_x_kernel<true, false, false>), grid, dim3(NT), 0, 0, p);
+      else if (var == 9) hipLaunchKernelGGL((gemm_planes_x_kernel<false, true, false>), grid, dim3(NT), 0, 0, p);
+      else if (var == 10) hipLaunchKernelGGL((gemm_planes_x_kernel<true, true, false>), grid, dim3(NT), 0, 0, p);
+      else if (var == 11) hipLaunchKernelGGL((gemm_planes_x_kernel<false, false, true>), grid, dim3(NT), 0, 0, p);
+      else if (var == 12) hipLaunchKernelGGL((gemm_planes_x_kernel<false, true, true>), grid, dim3(NT), 0, 0, p);
     };
     CK(hipMemset(dc, 0, (size_t)s.M * s.N * 4));
     launch();
@@ -605,7 +792,7 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const int reps = 20;
+    const int reps = 50;
     CK(hipEventRecord(e0));
     for (int i = 0; i < reps; ++i) launch();
     CK(hipEventRecord(e1));
@@ -616,6 +803,20 @@ int main(int argc, char** argv) {
     const double tf = 2.0 * s.M * s.N * s.K / (ms * 1e-3) / 1e12;
     printf("v%d %-50s M %5d N %5d K %5d tiles %4d  %.3f ms  %.1f TF/s fp32-equiv (%.3f of 416.7)\n", var,
            s.what, s.M, s.N, s.K, grid.x * grid.y, ms, tf, tf / 416.7);
+    if (var == 8 || var == 10) {  // in-kernel clock of the last launch: median over workgroups of dmemtime/drealtime
+      const int nwg = (int)(grid.x * grid.y) < 65536 ? (int)(grid.x * grid.y) : 65536;
+      std::vector<unsigned long long> h(4 * nwg);
+      CK(hipMemcpyFromSymbol(h.data(), HIP_SYMBOL(g_clk), h.size() * 8));
+      std::vector<double> f;
+      for (int w = 0; w < nwg; ++w) {
+        const double dt = (double)(h[4 * w + 3] - h[4 * w + 1]);
+        if (dt > 0) f.push_back((double)(h[4 * w + 2] - h[4 * w]) / dt * 0.1);  // GHz (realtime 100 MHz)
+      }
+      std::sort(f.begin(), f.end());
+      const double ghz = f.empty() ? 0 : f[f.size() / 2];
+      printf("   clock %.3f GHz (median of %zu workgroups): ceiling at that clock %.1f TF/s, this kernel %.3f of it\n",
+             ghz, f.size(), 416.7 * ghz / 2.4, tf / (416.7 * ghz / 2.4));
+    }
    }
     CK(hipFree(da));
     CK(hipFree(db));
