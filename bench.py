@@ -462,6 +462,15 @@ def main():
                             "frac": round(v[1] / (v[0] * 1e-3) / 1e12 / peak, 4) if v[0] else 0}
                         for k, v in by_tag.items()},
             "pmc": gemm_pmc(),
+            "dvfs": {
+                "note": ("the chip holds 1.79-2.09 GHz (not 2.4) in these MFMA-dense loops on random "
+                         "data: in-kernel s_memtime / s_memrealtime of the planes GEMM on the step's "
+                         "shapes (MI355X_MICROARCH.md, DVFS give-back). The instruction ceiling at that "
+                         "clock is 416.7 x clock / 2.4"),
+                "clock_GHz": [1.79, 2.09],
+                "ceiling_at_clock_TFps": [310.2, 362.9],
+                "source": "profiles/r06/gemm_planes_micro_stagger.txt (tools/micro/gemm_planes.hip v8/v10)",
+            },
         },
         "final_loss": round(final_loss, 5),
     }
