@@ -211,9 +211,6 @@ struct GP {
   long long psa, psb;  // plane strides (elements)
   int pld;             // row stride = padded K (a multiple of BK)
   int slab4;  // split-K slabs stored as dwordx4 rows (N % 4 == 0, M N < 2^29; store_slab4)
-  // conv / dgrad with the B operand pre-split channels-last (gemm_wc_kernel, round 6): B planes
-  // [3][B][Tr = Tn + 2][Cpad] (pB, plane stride psb); row of (b, t) for tap = b Tr + t + rs0 + rsd tap
-  int bcl, Cpad, Tr, rs0, rsd;
 };
 
 // Tile-order index -> (M tile, N tile): runs of GM M-tiles x all N-tiles, M fastest within a
@@ -1272,298 +1269,6 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_p_kernel(const GP p) {
   tile_pass_p<WG>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Conv / dgrad with the activation operand pre-split channels-last (round 6). In the 128 x 256
-// register-split kernel every thread loads, splits and stores both operands of each K tile: the
-// B operand (the activations, 256 rows x 32 channels per tile) is two thirds of that work, and
-// its source is time-contiguous (NCL), so it needs a transpose on the way into the [n][k] LDS
-// image. Here a pack kernel splits it ONCE per launch into three bf16 planes laid out as the LDS
-// image wants them, channels-last with one zero time step on each side of every batch row
-// ([plane][b][Tr = Tn + 2][Cpad], every concat source's crop offset and range mask applied, each
-// source's channels padded to whole 32-channel blocks as the A operand's K order has them), so a
-// K tile of B is 48 one-KB pieces moved by LDS-DMA: the tap's time shift is a whole-row offset
-// (rs0 + rsd tap rows), wave-uniform. The weights (A) keep the register split (their K order and
-// both orientations, W for conv and W^T for dgrad, are read as now).
-// The two 256-thread halves of the workgroup take different producer roles: waves 0-3 load,
-// split and store the A tile (all four units), waves 4-7 issue the B tile's 48 DMA pieces (12
-// each, inline asm: their own vmcnt counts only DMA, the A waves' only the compiler's loads).
-// Each SIMD holds one wave of each half, so the split VALU and the DMA issue run beside each
-// other's MFMAs. MFMA order, LDS image and epilogue are the 128 x 256 kernel's.
-struct ClArgs {  // pack of the conv B operand (see above)
-  __bf16* out;
-  long long ps;      // plane stride (elements) = B Tr Cpad
-  int Cpad, Tr, B, Tn, Tv, nb0;
-  const float* x0;
-  long long sb0;
-  int sc0, C0, T0, off0;
-  const float* x1;
-  long long sb1;
-  int sc1, C1, T1, off1;
-};
-
-// One workgroup per (64 padded time rows, 32 channels, b): 8 coalesced time samples per thread
-// in, an LDS transpose, 8 channels per thread out as three 16-byte plane stores.
-__global__ __launch_bounds__(256) void pack_cl_kernel(const ClArgs a) {
-  __shared__ float tile[32][65];
-  const int r0 = blockIdx.x * 64, c0 = blockIdx.y * 32, b = blockIdx.z;
-  const int tid = threadIdx.x;
-  {
-    const int ch = tid >> 3, rs = (tid & 7) * 8;
-    const int cp = c0 + ch;
-    const bool s1 = a.x1 != nullptr && cp >= a.nb0 * BK;
-    const int c = s1 ? cp - a.nb0 * BK : cp;
-    const int Cs = s1 ? a.C1 : a.C0, Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
-    const float* x = s1 ? a.x1 : a.x0;
-    const long long base = (long long)b * (s1 ? a.sb1 : a.sb0) + (long long)c * (s1 ? a.sc1 : a.sc0);
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int tin = r0 + rs + e - 1;  // padded row r holds input time r - 1
-      const bool ok = c < Cs && (unsigned)tin < (unsigned)a.Tv && (unsigned)(tin + off) < (unsigned)Ts;
-      v[e] = ok ? x[base + tin + off] : 0.f;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) tile[ch][rs + e] = v[e];
-  }
-  __syncthreads();
-  const int r = tid >> 2, cg = (tid & 3) * 8;
-  if (r0 + r >= a.Tr) return;
-  bf16x8 hi, mid, lo;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const Bf3 t3 = split1(tile[cg + i][r]);
-    hi[i] = t3.h;
-    mid[i] = t3.m;
-    lo[i] = t3.l;
-  }
-  __bf16* o = a.out + ((long long)b * a.Tr + r0 + r) * a.Cpad + c0 + cg;
-  *reinterpret_cast<bf16x8*>(o) = hi;
-  *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
-  *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
-}
-
-#ifndef MST_WC_VPM
-#define MST_WC_VPM 2
-#endif
-
-template <int AMODE>
-__device__ __forceinline__ void tile_pass_wc(const GP& p, float* lds, int m_t, int n_t, int kt0,
-                                             int kt1, int split, int tid) {
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int g = __builtin_amdgcn_readfirstlane(tid >> 8);  // 0: A producer, 1: B DMA
-  const int t = tid & 255;
-  const int wm = (wave >> 1) & 1, wn = wave & 1;
-  const int m0 = m_t * BM, n0 = n_t * BNW;
-  auto km_r = [&](int u) __attribute__((always_inline)) { return (t >> 3) + 32 * u; };
-  const int km_q = t & 7;
-  const int rm_row = t & 127;
-  const int kw = __builtin_amdgcn_readfirstlane((t >> 7) & 1);
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int r32 = lane & 31;
-  const int h = lane >> 5;
-  auto mfma_tile = [&](int buf) __attribute__((always_inline)) {
-    const __bf16* Ap = reinterpret_cast<const __bf16*>(lds) + buf * STAGE_BF;
-    const __bf16* Bp = Ap + 3 * PLANE;
-    const int ra0 = wm * 64 + r32, rb0 = 128 * g + wn * 64 + r32;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const Split3 b0 = ld_planes<PLANE_BW>(Bp, rb0, 2 * s + h), b1 = ld_planes<PLANE_BW>(Bp, rb0 + 32, 2 * s + h);
-      {
-        const Split3 a0 = ld_planes<PLANE>(Ap, ra0, 2 * s + h);
-        acc[0][0] = mfma_x6(a0, b0, acc[0][0]);
-        acc[0][1] = mfma_x6(a0, b1, acc[0][1]);
-      }
-      {
-        const Split3 a1 = ld_planes<PLANE>(Ap, ra0 + 32, 2 * s + h);
-        acc[1][0] = mfma_x6(a1, b0, acc[1][0]);
-        acc[1][1] = mfma_x6(a1, b1, acc[1][1]);
-      }
-    }
-  };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
-  if (kt0 < kt1) {
-    if (g == 0) {
-      // ---- A producer: the 128 x 256 kernel's A path with all four units in this half
-      f32x4 ra[2][4];
-      const rsrc_t rA = mk_rsrc(p.A, p.nA);
-      uint32_t rowA[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int m = m0 + (AMODE == 2 ? rm_row : km_r(u));
-        rowA[u] = m < p.M ? (uint32_t)(m * p.sAm + (AMODE == 2 ? 0 : 4 * km_q * p.sAc)) * 4u : OOB;
-      }
-      auto load_tile = [&](auto S, int tap, int blk) __attribute__((always_inline)) {
-        constexpr int st_ = decltype(S)::value;
-        const bool s1 = p.dual && blk >= p.nb0;
-        const int ci = (s1 ? blk - p.nb0 : blk) * BK + sel(s1, p.C0, 0);
-        const int sA = (ci * p.sAc + tap * p.sAt) * 4;
-        if constexpr (AMODE == 1) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) ra[st_][u] = ldbs4(rA, rowA[u], sA);
-        } else if constexpr (AMODE == 0) {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ra[st_][u][i] = ldbs(rA, rowA[u], sA + i * p.sAc * 4);
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              ra[st_][u][i] = ldbs(rA, rowA[0], sA + (4 * rm_quad(kw, u) + i) * p.sAc * 4);
-        }
-      };
-      auto store_tile = [&](auto S, int buf) __attribute__((always_inline)) {
-        constexpr int st = decltype(S)::value;
-        __bf16* Ap = reinterpret_cast<__bf16*>(lds) + buf * STAGE_BF;
-        if constexpr (AMODE == 2) {  // quads 2 kw + (0, 1): units (0, 1) and (2, 3)
-          split_store8<PLANE>(Ap, rm_row, 2 * kw, ra[st][0], ra[st][1]);
-          split_store8<PLANE>(Ap, rm_row, 2 * kw + 1, ra[st][2], ra[st][3]);
-        } else {
-#pragma unroll
-          for (int u = 0; u < 4; ++u) split_store4<PLANE>(Ap, km_r(u), km_q, ra[st][u]);
-        }
-      };
-      int tap = kt0 / p.nbT, blk = kt0 - tap * p.nbT;
-      auto advance = [&]() __attribute__((always_inline)) {
-        if (++blk == p.nbT) {
-          blk = 0;
-          ++tap;
-        }
-      };
-      load_tile(I0{}, tap, blk);
-      advance();
-      load_tile(I1{}, tap, blk);
-      advance();
-      store_tile(I0{}, 0);
-      __syncthreads();
-      auto step = [&](auto S) __attribute__((always_inline)) {
-        constexpr int sb = decltype(S)::value;
-        load_tile(S, tap, blk);  // tile i + 2 into the stage tile i left
-        advance();
-        mfma_tile(sb);
-        store_tile(std::integral_constant<int, sb ^ 1>{}, sb ^ 1);  // tile i + 1
-        constexpr int NV = AMODE == 1 ? 4 : 16;                        // VMEM loads per tile
-        constexpr int NS = AMODE == 2 ? 6 : 12;                        // LDS stores per tile
-#pragma unroll
-        for (int i = 0; i < 48; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-          if ((i + 1) * NV / 48 != i * NV / 48) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, MST_WC_VPM, 0);  // VALU (split)
-          if ((i + 1) * NS / 24 != i * NS / 24 && i < 24) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        }
-        __syncthreads();
-      };
-      for (int kt = kt0; kt < kt1; kt += 2) {
-        step(I0{});
-        if (kt + 1 < kt1) step(I1{});
-      }
-    } else {
-      // ---- B DMA: this wave's 12 of the tile's 48 one-KB pieces, j = (wave - 4) + 4 i: plane
-      // j / 16, tile rows 16 (j % 16) + lane / 4, LDS slot lane % 4 = quad q ^ pl_swz(row)
-      const int wv = wave - 4;
-      const rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)p.pB, (short)0, (int)(3 * p.psb * 2),
-                                                          0x00020000);
-      uint32_t voff[12];
-#pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        const int j = wv + 4 * i;
-        const int plane = j >> 4;
-        const int r = (j & 15) * 16 + (lane >> 2);
-        const int q = (lane & 3) ^ pl_swz(r);
-        const int n = n0 + r;
-        const int bb = n / p.Tn;
-        const long long e = plane * p.psb + ((long long)bb * p.Tr + (n - bb * p.Tn)) * p.Cpad + 8 * q;
-        voff[i] = n < p.N ? (uint32_t)(e * 2) : OOB;
-      }
-      const unsigned lds0 = (unsigned)(uintptr_t)lds + 3 * PLANE * 2;  // the B planes of stage 0
-      auto issue = [&](int buf, int kt) __attribute__((always_inline)) {
-        const int tap = kt / p.nbT, blk = kt - tap * p.nbT;
-        const int soff = ((p.rs0 + p.rsd * tap) * p.Cpad + blk * BK) * 2;
-#pragma unroll
-        for (int i = 0; i < 12; ++i) {
-          const unsigned dst =
-              __builtin_amdgcn_readfirstlane(lds0 + buf * STAGE_BF * 2 + (wv + 4 * i) * 1024);
-          dma_piece(rB, dst, voff[i], soff);
-        }
-      };
-      issue(0, kt0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (int kt = kt0; kt < kt1; ++kt) {
-        const int sb = (kt - kt0) & 1;
-        if (kt + 1 < kt1) issue(sb ^ 1, kt + 1);
-        mfma_tile(sb);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-    }
-  }
-
-  // ---- epilogue: accumulators -> LDS tile (128 x 256) -> row-contiguous stores
-  float* Cs = lds;
-  const int nl = tid & (BNW - 1);
-  const int n = n0 + nl;
-  __shared__ float s_bias_c[BM];
-  const bool use_bias = p.splitk <= 1 && p.bias != nullptr;
-  if (use_bias && tid < BM) s_bias_c[tid] = m0 + tid < p.M ? p.bias[m0 + tid] : 0.f;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int ml = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int nl2 = 128 * g + wn * 64 + j * 32 + r32;
-        Cs[ml * BNW + nl2] = acc[i][j][r];
-      }
-  __syncthreads();
-  if (p.slab4) {
-    store_slab4(p, Cs, m0, n0, split, tid);
-    return;
-  }
-  if (n < p.N) {
-    for (int ml = tid >> 8; ml < BM; ml += NTHRW / BNW) {
-      const int m = m0 + ml;
-      if (m >= p.M) break;
-      const float v = Cs[ml * BNW + nl];
-      if (p.splitk > 1) p.ws[((long long)split * p.M + m) * p.N + n] = v;
-      else conv_store_b(p, m, n, v, use_bias ? s_bias_c[ml] : 0.f);
-    }
-  }
-}
-
-template <int AMODE>
-__global__ __launch_bounds__(NTHRW, 1) void gemm_wc_kernel(const GP p) {
-  __shared__ __attribute__((aligned(16))) float lds[LDS_W_FLOATS];
-  const int nx = (p.N + BNW - 1) / BNW, ny = (p.M + BM - 1) / BM;
-  const int W = nx * ny * (int)gridDim.z;
-  const int t = xcd_order(blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z), W);
-  const int split = t / (nx * ny);
-  int m_t, n_t;
-  tile_of(t - split * nx * ny, nx, ny, m_t, n_t);
-  const int kt0 = (int)((long long)split * p.nk / p.splitk);
-  const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
-  tile_pass_wc<AMODE>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
-}
-
-static int gemm_bcl() {  // conv / dgrad on channels-last B planes; MST_GEMM_BCL=0: register split
-  static const int v = [] {
-    const char* e = getenv("MST_GEMM_BCL");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
-}
-
 static int wg_planes() {  // weight gradients on pre-split planes; MST_WG_PLANES=0: register split
   static const int v = [] {
     const char* e = getenv("MST_WG_PLANES");
@@ -1944,72 +1649,6 @@ int src_extent(GP& p, int B) {
   return MST_OK;
 }
 
-// Conv / dgrad on channels-last B planes (gemm_wc_kernel): stride-1 convolutions whose tap shift
-// is a whole padded time row (k3 convolutions and their input gradients, 1 x 1 linears), on the
-// 128 x 256 data-parallel / split-K schedule. The planes follow the split-K slabs in the workspace.
-void bcl_setup(GP& p, const mst_conv_desc* d) {
-  p.bcl = 0;
-  if (!gemm_bcl() || !p.wide || p.sk_L > 0 || d->a != 1 || d->ostride != 1) return;
-  int rs0, rsd;  // padded row of input time t + beta + g tap is t + rs0 + rsd tap
-  if (d->taps == 3 && d->g == 1 && d->beta == -1) rs0 = 0, rsd = 1;        // Conv1d k3 p1
-  else if (d->taps == 3 && d->g == -1 && d->beta == 1) rs0 = 2, rsd = -1;  // its input gradient
-  else if (d->taps == 1 && d->g == 0 && d->beta == 0) rs0 = 1, rsd = 0;    // Linear (NCL)
-  else return;
-  p.Cpad = p.nbT * BK;
-  p.Tr = d->Tn + 2;
-  const long long ps = (long long)d->B * p.Tr * p.Cpad;
-  if (6 * ps >= (long long)OOB || (long long)p.Tr * p.Cpad * d->B >= (1ll << 31)) return;
-  p.psb = ps;
-  p.rs0 = rs0;
-  p.rsd = rsd;
-  p.bcl = 1;
-}
-
-size_t bcl_slab_bytes(const GP& p) { return (sched_ws_bytes(p) + 255) / 256 * 256; }
-size_t bcl_plane_bytes(const GP& p) { return ((size_t)6 * p.psb + 255) / 256 * 256; }
-size_t conv_ws_bytes(const GP& p) { return p.bcl ? bcl_slab_bytes(p) + bcl_plane_bytes(p) : sched_ws_bytes(p); }
-
-ClArgs cl_args(const GP& p, const mst_conv_desc* d) {
-  ClArgs a{};
-  a.out = const_cast<__bf16*>(p.pB);
-  a.ps = p.psb;
-  a.Cpad = p.Cpad;
-  a.Tr = p.Tr;
-  a.B = d->B;
-  a.Tn = d->Tn;
-  a.Tv = d->Tv;
-  a.nb0 = p.nb0;
-  a.x0 = p.x0;
-  a.sb0 = p.sb0;
-  a.sc0 = p.sc0;
-  a.C0 = p.C0;
-  a.T0 = p.T0;
-  a.off0 = p.off0;
-  a.x1 = p.dual ? p.x1 : nullptr;
-  a.sb1 = p.sb1;
-  a.sc1 = p.sc1;
-  a.C1 = p.C1;
-  a.T1 = p.T1;
-  a.off1 = p.off1;
-  return a;
-}
-
-int launch_bcl(const GP& p, const mst_conv_desc* d, hipStream_t st) {
-  const ClArgs a = cl_args(p, d);
-  hipLaunchKernelGGL(pack_cl_kernel, dim3(ceil_div(p.Tr, 64), p.Cpad / BK, d->B), dim3(256), 0, st, a);
-  MST_CHECK_LAUNCH();
-  const dim3 grid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk), block(NTHRW);
-  if (p.a_mode == 1) hipLaunchKernelGGL((gemm_wc_kernel<1>), grid, block, 0, st, p);
-  else if (p.a_mode == 2) hipLaunchKernelGGL((gemm_wc_kernel<2>), grid, block, 0, st, p);
-  else hipLaunchKernelGGL((gemm_wc_kernel<0>), grid, block, 0, st, p);
-  MST_CHECK_LAUNCH();
-  if (p.splitk > 1) {
-    launch_reduce<false>(p, st);
-    MST_CHECK_LAUNCH();
-  }
-  return MST_OK;
-}
-
 int build_conv(const mst_conv_desc* d, GP& p) {
   MST_REQUIRE(d && d->A && d->src[0].p && d->dst[0].p);
   MST_REQUIRE(d->B > 0 && d->M > 0 && d->Tn > 0 && d->Ctot > 0 && taps_ok(d->taps));
@@ -2068,7 +1707,6 @@ int build_conv(const mst_conv_desc* d, GP& p) {
   p.seed_dev = reinterpret_cast<const unsigned long long*>(d->seed_dev);
   p.wide = gemm_wide();
   choose_sched(p, d->splitk);
-  bcl_setup(p, d);
   return MST_OK;
 }
 
@@ -2305,20 +1943,14 @@ int mst_gemm_products(void) { return 6; }
 size_t mst_conv_fwd_workspace_size(const mst_conv_desc* d) {
   GP p;
   if (build_conv(d, p) != MST_OK) return 0;
-  return conv_ws_bytes(p);
+  return sched_ws_bytes(p);
 }
 
 int mst_conv_fwd_f32(const mst_conv_desc* d, float* ws, size_t ws_bytes, void* stream) {
   GP p;
   int rc = build_conv(d, p);
   if (rc) return rc;
-  // channels-last B planes when the caller's workspace holds them (else the register split)
-  if (p.bcl && (!ws || ((uintptr_t)ws & 255) || ws_bytes < conv_ws_bytes(p))) p.bcl = 0;
   bind_ws(p, ws, ws_bytes);
-  if (p.bcl) {
-    p.pB = reinterpret_cast<const __bf16*>(reinterpret_cast<char*>(ws) + bcl_slab_bytes(p));
-    return launch_bcl(p, d, (hipStream_t)stream);
-  }
   return launch<false>(p, (hipStream_t)stream, d->taps);
 }
 

@@ -19,7 +19,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 KNOBS = [
     {"MST_GEMM_WIDE": "0"},         # conv / dgrad on the 128 x 128 kernel
-    {"MST_GEMM_BCL": "0"},          # conv / dgrad with both operands split in registers
     {"MST_GEMM_SCHED": "sk"},       # stream-K for every GEMM
     {"MST_SPLITK_TAU": "1e-9"},     # split-K cost model pushed to no split
     {"MST_SLAB4": "0"},             # split-K slabs stored element by element
