@@ -14,6 +14,8 @@ Usage:  python tests/golden/make_golden.py          (blocks, B=2/T=44, B=1/T=252
         python tests/golden/make_golden.py bench    (B=32/T=252, the benchmarked config)
         python tests/golden/make_golden.py t860     (B=2/T=860, the reference's own training
                                                      chunk, and B=2/T=100, an off-grid length)
+        python tests/golden/make_golden.py b16t860  (B=16/T=860: the reference's default batch,
+                                                     train.py:219, on that chunk)
 """
 import os
 import sys
@@ -288,6 +290,9 @@ if __name__ == "__main__":
     if sys.argv[1:] == ["t860"]:  # the reference's training chunk (preprocess.py:42,66) + off-grid T
         full_model_lowmem(2, 860, "full_B2_T860.npz")
         full_model_lowmem(2, 100, "full_B2_T100.npz")
+        sys.exit(0)
+    if sys.argv[1:] == ["b16t860"]:  # the reference's default batch (train.py:219) on that chunk
+        full_model_lowmem(16, 860, "full_B16_T860.npz")
         sys.exit(0)
     blocks()
     full_model(2, 44, "full_B2_T44.npz")

@@ -492,14 +492,19 @@ def test_full_model_reference_lengths(cuda, fname):
 
 def test_train_steps_reference_batch_B16_T860(cuda):
     """The reference's default training shape: --batch-size 16 (train.py:219) on 860-frame
-    chunks (preprocess.py:42,66). Properties, since no CPU reference fits a GPU test's time at
-    this size: samples are independent (InstanceNorm is per sample, train.py:132's L1 is a mean),
-    so the B = 16 loss equals the mean of its two B = 8 halves' losses (1e-5 relative) and its
-    weight gradients the mean of theirs. The halves run other split-K schedules, i.e. other fp32
-    summation orders, and this network's fp32 gradients are ill-conditioned (L1 sign, ReLU /
-    LeakyReLU kinks, maxpool ties flip under rounding), so each parameter's rel L2 gap is held to
-    4x the reference's own fp32-vs-fp64 gap for that parameter at T = 860 (full_B2_T860.npz),
-    floor 1e-3. Then three Adam steps on the batch stay finite and lower the loss."""
+    chunks (preprocess.py:42,66).
+    Against the reference itself (round 6): full_B16_T860.npz (make_golden.py b16t860:
+    /root/reference/model/model.py in fp32 and fp64 on these 16 detinit samples, eval mode) with
+    test_full_model_bench_config_B32's bounds: loss 1e-4 relative, sampled outputs within 1e-4 of
+    the output scale and 1e-4 relative L2 vs fp64, sampled weight gradients within 4x the
+    reference's own fp32-vs-fp64 gap per parameter.
+    Properties on top: samples are independent (InstanceNorm is per sample, train.py:132's L1 is
+    a mean), so the B = 16 loss equals the mean of its two B = 8 halves' losses (1e-5 relative)
+    and its weight gradients the mean of theirs. The halves run other split-K schedules, i.e.
+    other fp32 summation orders, and this network's fp32 gradients are ill-conditioned (L1 sign,
+    ReLU / LeakyReLU kinks, maxpool ties flip under rounding), so each parameter's rel L2 gap is
+    held to 4x the reference's own fp32-vs-fp64 gap for that parameter at T = 860 (full_B2_T860
+    .npz), floor 1e-3. Then three Adam steps on the batch stay finite and lower the loss."""
     from ml_music_style_transfer_amd import engine as E
     from ml_music_style_transfer_amd.train import make_optimizer
     B, T = 16, 860
@@ -508,8 +513,15 @@ def test_train_steps_reference_batch_B16_T860(cuda):
     grads, losses = [], []
     for sl in (slice(0, B), slice(0, B // 2), slice(B // 2, B)):
         net.zero_grad(set_to_none=True)
-        loss = E.l1_loss(net(xm[sl], xa[sl], cd[sl]), tg[sl])
+        y = net(xm[sl], xa[sl], cd[sl])
+        loss = E.l1_loss(y, tg[sl])
         loss.backward()
+        if sl.start == 0 and sl.stop == B:
+            err, rel, worst_ref = _full_vs_fp64(net, np.load(os.path.join(GOLD, "full_B16_T860.npz")),
+                                                y, loss)
+            print(f"B=16 T=860 vs the reference: out max {err:.3e}, rel L2 {rel:.3e}; worst "
+                  f"(ratio to ref fp32 gap, ours, ref fp32 gap, name) {worst_ref}")
+        del y
         losses.append(loss.item())
         grads.append({n: p.grad.detach().double().clone() for n, p in net.named_parameters()
                       if p.grad is not None})
