@@ -211,6 +211,8 @@ struct GP {
   long long psa, psb;  // plane strides (elements)
   int pld;             // row stride = padded K (a multiple of BK)
   int slab4;  // split-K slabs stored as dwordx4 rows (N % 4 == 0, M N < 2^29; store_slab4)
+  int b2;     // weight-gradient B planes in two copies (build_wgrad_planes); bC: channels
+  int bC;
 };
 
 // Tile-order index -> (M tile, N tile): runs of GM M-tiles x all N-tiles, M fastest within a
@@ -943,6 +945,8 @@ struct PackArgs {
   const float* x1;
   long long sb1;
   int sc1, T1, off1;
+  int two;  // k3 weight gradient in two copies (see build_wgrad_planes): tap 1 in rows [0, C),
+            // taps 0 and 2 in rows [C, 2C) (tap 2 read 2 elements further on), zero row 2C
 };
 
 // One thread per (channel, 8 consecutive k), grid-stride over channels x ld/8 items (short rows,
@@ -957,10 +961,18 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
   const rsrc_t r1 = a.x1 ? mk_rsrc(a.x1, (long long)(a.B - 1) * a.sb1 +
                                              (long long)(chans - a.C0 - 1) * a.sc1 + a.T1)
                          : r0;
-  const int total = chans * q8;  // < 2^31: checked by the host (32-bit index math: a 64-bit
-                                 // division per item made the pack 30 % slower)
+  const int total = (chans + a.two) * q8;  // < 2^31: checked by the host (32-bit index math: a
+                                           // 64-bit division per item made the pack 30 % slower)
   for (int it = blockIdx.x * 256 + threadIdx.x; it < total; it += gridDim.x * 256) {
     const int c = it / q8, kq = it - c * q8;
+    if (c == chans) {  // the two-copy layout's zero row (what tap 2's shifted reads run into)
+      __bf16* o = a.out + (long long)(2 * chans) * a.ld + 8 * kq;
+      const bf16x8 z = {};
+      *reinterpret_cast<bf16x8*>(o) = z;
+      *reinterpret_cast<bf16x8*>(o + a.ps) = z;
+      *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = z;
+      continue;
+    }
     const bool s1 = c >= a.C0;
     const int cs = s1 ? c - a.C0 : c;
     const int Ts = s1 ? a.T1 : a.T0, off = s1 ? a.off1 : a.off0;
@@ -1028,18 +1040,21 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
       sp[9] = split1(hr);
 #pragma unroll
       for (int tap = 0; tap < 3; ++tap) {  // unrolled: sp[] stays in registers
-        if (tap >= ntap) break;
+        if (tap >= ntap || (a.two && tap == 2)) break;
         bf16x8 hi, mid, lo;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const bool ok = t0 + e < a.Tk;  // time padding
+          // time padding; the two-copy layout's tap-0 copy also holds t = Tk (tap 2 reads it
+          // two elements on, at t = Tk - 2)
+          const bool ok = t0 + e < a.Tk + (a.two && tap == 0);
           // taps 3: window element e + tap (u = t0 - 1 + tap + e); taps 1: own element e
           const Bf3 v = ntap == 3 ? sp[e + tap] : sp[e + 1];
           hi[e] = ok ? v.h : (__bf16)0.f;
           mid[e] = ok ? v.m : (__bf16)0.f;
           lo[e] = ok ? v.l : (__bf16)0.f;
         }
-        __bf16* o = a.out + (long long)(c * ntap + tap) * a.ld + k0;
+        const int orow = a.two ? (tap == 1 ? c : chans + c) : c * ntap + tap;
+        __bf16* o = a.out + (long long)orow * a.ld + k0;
         *reinterpret_cast<bf16x8*>(o) = hi;
         *reinterpret_cast<bf16x8*>(o + a.ps) = mid;
         *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
@@ -1141,7 +1156,12 @@ __device__ __forceinline__ void tile_pass_p(const GP& p, char* lds, int m_t, int
     const int q = (lane & 3) ^ pl_swz(r);
     const int row = (a ? m0 : n0) + r;
     const bool in = row < (a ? p.M : p.N);
-    const long long e = plane * (a ? p.psa : p.psb) + (long long)row * p.pld + 8 * q;
+    // two-copy B planes: row n = 3 c + tap reads copy row c (tap 1) or C + c (taps 0, 2), tap 2
+    // two elements (4 bytes: dword-aligned) further along k
+    const int c3 = row / 3, tp = row - 3 * c3;
+    const int srow = (!a && p.b2) ? (tp == 1 ? c3 : p.bC + c3) : row;
+    const int eoff = (!a && p.b2 && tp == 2) ? 2 : 0;
+    const long long e = plane * (a ? p.psa : p.psb) + (long long)srow * p.pld + 8 * q + eoff;
     voff[i] = in ? (uint32_t)(e * 2) : OOB;
   }
   const unsigned lds0 = (unsigned)(uintptr_t)lds;  // LDS byte address (low half of the flat one)
@@ -1267,6 +1287,14 @@ __global__ __launch_bounds__(NTHRW, 1) void gemm_p_kernel(const GP p) {
   const int kt0 = (int)((long long)split * p.nk / p.splitk);
   const int kt1 = (int)((long long)(split + 1) * p.nk / p.splitk);
   tile_pass_p<WG>(p, lds, m_t, n_t, kt0, kt1, split, threadIdx.x);
+}
+
+static int wg_two_copy() {  // k3 weight-gradient B planes in two copies; MST_WG_TWO=0: three
+  static const int v = [] {
+    const char* e = getenv("MST_WG_TWO");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
 }
 
 static int wg_planes() {  // weight gradients on pre-split planes; MST_WG_PLANES=0: register split
@@ -1818,7 +1846,16 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
   p.K = (int)Kp;
   p.nk = (int)(Kp / BK);
   p.psa = (long long)p.M * Kp;
-  p.psb = (long long)p.N * Kp;
+  // k3 convolutions' weight gradient (unit stride, the pack's fast path) with at least one
+  // padding step after each batch row (Tp > Tk): the three tap-shifted copies of X become two,
+  // tap 1 and tap 0 (= tap 2 read two elements further: 4 bytes, which LDS-DMA takes), 12 instead
+  // of 18 bytes per element written by the pack and fetched by the GEMM. A shifted read that runs
+  // past a batch row lands on the next row's leading zero (valid t) or meets dY = 0 (padding t),
+  // and past a channel's last row on the next channel's leading zero or the zero row 2C.
+  p.b2 = wg_two_copy() && d->taps == 3 && d->a == 1 && d->g == 1 && d->beta == -1 && d->Tv <= Tp &&
+         Tp > d->Tk;
+  p.bC = d->Ctot;
+  p.psb = p.b2 ? (long long)(2 * d->Ctot + 1) * Kp : (long long)p.N * Kp;
   // the plane descriptors address 3 planes with 32-bit byte offsets
   MST_REQUIRE(6 * p.psa < (long long)OOB && 6 * p.psb < (long long)OOB);
   p.out = d->out;
@@ -1855,6 +1892,7 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
   PackArgs& b = w.pb;
   b = a;
   b.ps = p.psb;
+  b.two = p.b2;
   b.rows = p.N;
   b.taps = d->taps;
   b.a = d->a;
@@ -1888,7 +1926,7 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
 }
 
 int launch_pack(const PackArgs& a, hipStream_t st) {
-  const long long items = (long long)(a.rows / a.taps) * (a.ld >> 3);
+  const long long items = (long long)(a.rows / a.taps + a.two) * (a.ld >> 3);
   long long blocks = (items + 255) / 256;
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);

@@ -23,6 +23,7 @@ KNOBS = [
     {"MST_SPLITK_TAU": "1e-9"},     # split-K cost model pushed to no split
     {"MST_SLAB4": "0"},             # split-K slabs stored element by element
     {"MST_REDUCE_ROWS": "0"},       # split-K reduce as a 1-D float4 grid (a division per element)
+    {"MST_WG_TWO": "0"},            # k3 wgrad B planes in three tap copies instead of two
     {"MST_WG_PLANES": "0"},         # wgrad on the register-split 128 x 128 kernel (K classes)
     {"MST_WG_PLANES": "0", "MST_WG_VEC": "0"},  # ... with dword loads in the unmasked classes too
     {"MST_IN_SEG": "0"},            # one InstanceNorm row per wave
