@@ -954,7 +954,7 @@ struct PackArgs {
 // c taps + tap) from one read of the source. Loads are raw buffer loads through one descriptor
 // per source; an element outside its ranges (t >= Tk, b >= B, input time outside [0, Tv) or the
 // source) gets the OOB offset: hardware zero, no branches.
-__global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
+__device__ __forceinline__ void pack_body(const PackArgs& a, int bid, int nblk) {
   const int q8 = a.ld >> 3;
   const int chans = a.rows / a.taps;
   const rsrc_t r0 = mk_rsrc(a.x0, (long long)(a.B - 1) * a.sb0 + (long long)(a.C0 - 1) * a.sc0 + a.T0);
@@ -963,7 +963,7 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
                          : r0;
   const int total = (chans + a.two) * q8;  // < 2^31: checked by the host (32-bit index math: a
                                            // 64-bit division per item made the pack 30 % slower)
-  for (int it = blockIdx.x * 256 + threadIdx.x; it < total; it += gridDim.x * 256) {
+  for (int it = bid * 256 + threadIdx.x; it < total; it += nblk * 256) {
     const int c = it / q8, kq = it - c * q8;
     if (c == chans) {  // the two-copy layout's zero row (what tap 2's shifted reads run into)
       __bf16* o = a.out + (long long)(2 * chans) * a.ld + 8 * kq;
@@ -1102,6 +1102,13 @@ __global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a) {
       *reinterpret_cast<bf16x8*>(o + 2 * a.ps) = lo;
     }
   }
+}
+
+// Both operands' packs of one weight gradient in ONE launch (blocks [0, nba) pack A, the rest B):
+// one launch fewer per layer on the weight-gradient stream.
+__global__ __launch_bounds__(256) void pack_planes_kernel(const PackArgs a, const PackArgs b, int nba) {
+  if ((int)blockIdx.x < nba) pack_body(a, blockIdx.x, nba);
+  else pack_body(b, blockIdx.x - nba, gridDim.x - nba);
 }
 
 constexpr int STAGE_P = STAGE_BF;  // 72 KB of bf16 per stage: A 3 x [128][32], B 3 x [256][32]
@@ -1925,11 +1932,15 @@ int build_wgrad_planes(const mst_wgrad_desc* d, PlanesWG& w) {
   return MST_OK;
 }
 
-int launch_pack(const PackArgs& a, hipStream_t st) {
+static unsigned pack_blocks(const PackArgs& a) {
   const long long items = (long long)(a.rows / a.taps + a.two) * (a.ld >> 3);
   long long blocks = (items + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(pack_planes_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  return (unsigned)(blocks > 8192 ? 8192 : blocks);
+}
+
+int launch_pack2(const PackArgs& a, const PackArgs& b, hipStream_t st) {
+  const unsigned na = pack_blocks(a), nb = pack_blocks(b);
+  hipLaunchKernelGGL(pack_planes_kernel, dim3(na + nb), dim3(256), 0, st, a, b, (int)na);
   MST_CHECK_LAUNCH();
   return MST_OK;
 }
@@ -1942,9 +1953,7 @@ int run_wgrad_planes(PlanesWG& w, float* ws, hipStream_t st) {
   w.pb.out = reinterpret_cast<__bf16*>(base + w.slab_bytes + w.a_bytes);
   p.pA = w.pa.out;
   p.pB = w.pb.out;
-  int rc = launch_pack(w.pa, st);
-  if (rc) return rc;
-  rc = launch_pack(w.pb, st);
+  int rc = launch_pack2(w.pa, w.pb, st);
   if (rc) return rc;
   dim3 grid(ceil_div(p.N, BNW), ceil_div(p.M, BM), p.splitk);
   hipLaunchKernelGGL((gemm_p_kernel<true>), grid, dim3(NTHRW), 0, st, p);
