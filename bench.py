@@ -432,7 +432,8 @@ def main():
             "bound": "mfma",
             "kernel": ("gemm_w_kernel (128 x 256 tiles: conv/linear fwd and dgrad, operands split in "
                        "registers) and gemm_p_kernel (128 x 256: wgrad on operand planes pre-split by "
-                       "pack_planes_kernel, split-K) (implicit GEMM; fp32 operands "
+                       "pack_planes_kernel, LDS-DMA, the second wave per SIMD staggered, split-K) "
+                       "(implicit GEMM; fp32 operands "
                        + ("split into 3 bf16 pieces, 6 x v_mfma_f32_32x32x16_bf16 per 16-deep k step)"
                           if products > 1 else "v_mfma_f32_32x32x2_f32)")),
             "achieved": round(achieved, 2),
