@@ -96,7 +96,9 @@ def test_performancenet_step_with_mss_loss(cuda, phase):
     dS = S.grad.double().cpu()
     rel_out = ((dS - dS64).norm() / dS64.norm()).item()
     gap_out = ((dS32.double() - dS64).norm() / dS64.norm()).item()
-    assert rel_out <= max(2 * gap_out, 2e-2), (rel_out, gap_out)
+    # bound: 4x torch fp32's own gap, floor 1e-4 (measured: 2.6e-5 / 2.9e-6 against torch fp32's
+    # 9.6e-6 / 5.2e-6, profiles/r06/pytest_gpu_r6h.log; round 5 floored this at 2 %)
+    assert rel_out <= max(4 * gap_out, 1e-4), (rel_out, gap_out)
     worst = []
     for n, q in net.named_parameters():
         if q.grad is None or g64.get(n) is None:
@@ -110,11 +112,17 @@ def test_performancenet_step_with_mss_loss(cuda, phase):
         if n.endswith(".bias") and not (n.startswith("dense_concats") or n == "lastconv.bias"):
             continue  # conv biases followed by InstanceNorm: exact gradient 0 (rounding noise only)
         worst.append((e_ours, e_ref, n))
-        assert e_ours <= max(4 * e_ref, 2e-2), (n, e_ours, e_ref)
+        # 4x torch fp32's own gap for the parameter, floor 1e-3 (round 5: 2e-2); no parameter's
+        # torch fp32 gap is below 2.5e-3 here (profiles/r06/pytest_gpu_mss_train_s6b.log), so the
+        # floor binds nowhere: the bound is the reference-gap rule alone
+        assert e_ours <= max(4 * e_ref, 1e-3), (n, e_ours, e_ref)
     opt = make_optimizer(net, lr=1e-3)
     opt.step()
     assert all(torch.isfinite(q).all() for q in net.parameters())
     worst.sort()
+    floored = [w for w in worst if 4 * w[1] < 1e-3]
+    print(f"phase={phase}: {len(floored)} of {len(worst)} parameters under the 1e-3 floor, the "
+          f"largest of ours there {max((w[0] for w in floored), default=0):.2e}")
     print(f"phase={phase}: loss {loss.item():.6f} vs fp64 {l64:.6f} (fp32 CPU {l32:.6f}); "
           f"dL/dS rel L2 {rel_out:.2e} (torch fp32 {gap_out:.2e}); worst weight-gradient gaps (ours, torch fp32, name) {worst[-3:]}")
 
