@@ -433,85 +433,118 @@ __device__ __forceinline__ d2 twd(const d2* qt, int m, int N) {
   return dk(neg ? -a : a, neg ? -b : b);
 }
 
-// LDS slot of complex element i of a wave buffer: an XOR-linear swizzle of the low 4 index bits
-// by bits 3..8, found by exhaustive local search over such swizzles against the bank rules of
-// ds_read_b128 (16-lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31}, 16 slots per 256-B row)
-// and ds_write_b128 (8 contiguous lanes, 8 slots per 128-B row) for every access of the loads,
-// the Stockham stages and the post-twist at n = 64 .. 2048 (model and search:
-// tools/lds_swizzle_search.py): 2604 -> 1004 modelled conflict cycles per wave pass; PMC before
-// it: 7.4 conflict cycles per LDS instruction (profiles/r05/pmc_mss_r5h_summary.txt).
-#ifndef MST_TSW
-#define MST_TSW 2  // A/B: 0 identity, 1 i ^ ((i >> 3) & 7) (1537 modelled cycles), 2 the searched one
+// LDS slot of complex element i of a wave buffer: slot = i ^ h(i), h linear over bits 3..10 of i
+// (each bit's vector flips only lower bits, so this is a bijection). Found by local search over
+// such swizzles against the ds_read_b128 bank rule (16-lane groups {0-3,12-15,20-27} /
+// {4-11,16-19,28-31}, 16 slots per 256-B row) and the ds_write_b128 rule (8 contiguous lanes, 8
+// slots per 128-B row) for every access of the register-first radix-8 schedule below at n = 64 ..
+// 2048 (tools/lds_swizzle_search.py): 956 modelled conflict cycles over 372 LDS instructions per
+// wave pass of every size, against 1004 over 644 for the round-5 radix-4 schedule with its own
+// searched swizzle. Linear: tsw(a | b) = tsw(a) ^ tsw(b) for disjoint bits, so the loops form one
+// lane-dependent slot and XOR compile-time constants into it.
+__device__ __forceinline__ constexpr int tsw(int i) {
+  constexpr int V[8] = {4, 1, 3, 12, 11, 4, 0, 2};  // bits 3 .. 10
+  int h = 0;
+  for (int b = 0; b < 8; ++b) h ^= (-((i >> (b + 3)) & 1)) & V[b];
+  return i ^ h;
+}
+
+// a W_R^k for a compile-time k < R / 2 (R | 16): exact forms for 1, -i and (+-1 - i) / sqrt 2
+template <int R>
+__device__ __forceinline__ d2 wconst(d2 a, int k) {
+  if (k == 0) return a;
+  if (4 * k == R) return dk(a.y, -a.x);
+  constexpr double h = 0.70710678118654752440;
+  if (8 * k == R) return dk(h * (a.x + a.y), h * (a.y - a.x));
+  if (8 * k == 3 * R) return dk(h * (a.y - a.x), -h * (a.x + a.y));
+  const int m = k * (2048 / R), q = m >> 9;  // W2048^m = (-i)^q W2048^(m mod 512)
+  const double2 w = kMssW2048d.w[m & 511];
+  const d2 t = q ? dk(w.y, -w.x) : dk(w.x, w.y);
+  return dmul(a, t);
+}
+
+// W_R^r = (cos, -sin)(2 pi r / R) for a compile-time r < R (R | 2048), from the float64 table
+template <int R>
+__device__ __forceinline__ d2 wturn(int r) {
+  const int m = r * (2048 / R), q = m >> 9;  // W2048^m = (-i)^q W2048^(m mod 512)
+  const double2 w = kMssW2048d.w[m & 511];
+  const double a = (q & 1) ? w.y : w.x, b = (q & 1) ? -w.x : w.y;
+  return (q & 2) ? dk(-a, -b) : dk(a, b);
+}
+
+// forward DFT of R = 2^k points in registers, natural order (radix-2 decimation in time)
+template <int R>
+__device__ __forceinline__ void dft_d(d2 (&v)[R]) {
+  if constexpr (R == 1) {
+    return;
+  } else if constexpr (R == 2) {
+    const d2 a = v[0], b = v[1];
+    v[0] = a + b;
+    v[1] = a - b;
+  } else {
+    d2 e[R / 2], o[R / 2];
+#pragma unroll
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
+    }
+    dft_d<R / 2>(e);
+    dft_d<R / 2>(o);
+#pragma unroll
+    for (int k = 0; k < R / 2; ++k) {
+      const d2 t = wconst<R>(o[k], k);
+      v[k] = e[k] + t;
+      v[k + R / 2] = e[k] - t;
+    }
+  }
+}
+
+// One Stockham radix-R stage of the BWT / M transforms of size M in place in s (Ns = product of
+// the earlier stages' radices): every input of the wave read to registers, then written
+template <int R, int M, int BWT, int Ns>
+__device__ __forceinline__ void stage_d(d2* s, const d2* qt, int lane) {
+  constexpr int NR = M / R, IT = BWT / R / 64;
+  static_assert(IT >= 1, "a stage needs every lane");
+  d2 v[IT][R];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
+    const int pb = tsw(fr * M + j);
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[it][r] = s[pb ^ tsw(r * NR)];
+  }
+  wave_sync();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR, k = j & (Ns - 1);
+    const d2 w1 = twd(qt, k, Ns * R);
+    d2 w = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      v[it][r] = dmul(v[it][r], w);
+      if (r + 1 < R) w = dmul(w, w1);
+    }
+    dft_d<R>(v[it]);
+    const int pb = tsw(fr * M + (j - k) * R + k);
+#pragma unroll
+    for (int r = 0; r < R; ++r) s[pb ^ tsw(r * Ns)] = v[it][r];
+  }
+  wave_sync();
+}
+
+// the stages after the first: radix 8 while 8 divides what is left, then the remainder (2 or 4)
+template <int M, int BWT, int Ns>
+__device__ __forceinline__ void stages_d(d2* s, const d2* qt, int lane) {
+  if constexpr (Ns < M) {
+    constexpr int R = M / Ns < 8 ? M / Ns : 8;
+    stage_d<R, M, BWT, Ns>(s, qt, lane);
+    stages_d<M, BWT, Ns * R>(s, qt, lane);
+  }
+}
+
+#ifndef MSS_R16
+#define MSS_R16 1  // n = 2048: a radix-16 first stage (5 VGPRs spilled; radix 8 spills 38)
 #endif
-__device__ __forceinline__ int tsw(int i) {
-  if constexpr (MST_TSW == 0) return i;
-  if constexpr (MST_TSW == 1) return i ^ ((i >> 3) & 7);
-  const int t = i >> 3;
-  const int b0 = t & 1, b12 = ((t >> 1) ^ (t >> 2)) & 1, b4 = (t >> 4) & 1, b5 = (t >> 5) & 1;
-  return i ^ (b0 ^ b5 ^ (-b12 & 15) ^ (-b4 & 9));
-}
-
-// FB transforms of size N = 2^LOG2N in place in s[0 .. FB N) (Stockham, natural-order result);
-// element i lives at slot tsw(i)
-template <int LOG2N, int BWT>
-__device__ __forceinline__ void wave_fft_d(d2* s, const d2* qt, int lane) {
-  constexpr int N = 1 << LOG2N, NR = N / 4, IT = BWT / 4 / 64;
-  int Ns = 1;
-#pragma unroll
-  for (int st = 0; st < LOG2N / 2; ++st) {
-    d2 v[IT][4];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[it][r] = s[tsw(fr * N + j + r * NR)];
-    }
-    wave_sync();
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = lane + 64 * it, fr = idx / NR, j = idx - fr * NR;
-      const int k = j & (Ns - 1);
-      if (st > 0) {
-        const d2 w1 = twd(qt, k, 4 * Ns), w2 = dmul(w1, w1), w3 = dmul(w2, w1);
-        v[it][1] = dmul(v[it][1], w1);
-        v[it][2] = dmul(v[it][2], w2);
-        v[it][3] = dmul(v[it][3], w3);
-      }
-      const d2 t0 = v[it][0] + v[it][2], t1 = v[it][0] - v[it][2];
-      const d2 t2 = v[it][1] + v[it][3], t3 = v[it][1] - v[it][3];
-      const d2 it3 = dk(-t3.y, t3.x);
-      const int d = fr * N + (j - k) * 4 + k;
-      s[tsw(d)] = t0 + t2;
-      s[tsw(d + Ns)] = t1 - it3;
-      s[tsw(d + 2 * Ns)] = t0 - t2;
-      s[tsw(d + 3 * Ns)] = t1 + it3;
-    }
-    wave_sync();
-    Ns *= 4;
-  }
-  if constexpr (LOG2N & 1) {
-    constexpr int NR2 = N / 2, IT2 = BWT / 2 / 64;
-    d2 v[IT2][2];
-#pragma unroll
-    for (int it = 0; it < IT2; ++it) {
-      const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
-      v[it][0] = s[tsw(fr * N + j)];
-      v[it][1] = s[tsw(fr * N + j + NR2)];
-    }
-    wave_sync();
-#pragma unroll
-    for (int it = 0; it < IT2; ++it) {
-      const int idx = lane + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
-      const int k = j & (Ns - 1);
-      const d2 b = dmul(v[it][1], twd(qt, k, 2 * Ns));
-      const int d = fr * N + (j - k) * 2 + k;
-      s[tsw(d)] = v[it][0] + b;
-      s[tsw(d + Ns)] = v[it][0] - b;
-    }
-    wave_sync();
-  }
-}
-
 constexpr int MSS_TW = 4;           // waves per target workgroup
 constexpr int MSS_TBW = 512;        // complex doubles per wave buffer (n/2 <= 512); n = 2048: 1024
 constexpr int MSS_TROUNDS = 4;      // frame batches per wave per workgroup
@@ -546,32 +579,59 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
   const float* x = A.target + (long long)b * A.L;
   float* out = A.tmag[z] + (long long)b * T * NBIN;
   constexpr int PER_WG = MSS_TW * FBT * MSS_TROUNDS;
+  // The first FFT stage runs on the loaded samples in registers (no LDS pass for the load):
+  // radix R1 over the FBT frames' z_j = w_2j x_2j + i w_2j+1 x_2j+1 (periodic Hann in float64,
+  // reflect pad), lane element (u, j) takes c = j + r NR1, r < R1. The window's angles there are
+  // 2 pi (2j + {0, 1}) / N + 2 pi r / R1: the lane keeps cos / sin of its two base angles and
+  // rotates them by compile-time constants (float64 angle sums, no table reads per batch).
+  constexpr int R1 = (MSS_R16 && BWT >= 1024 && HALF >= 1024) ? 16 : (HALF < 8 ? HALF : 8);
+  constexpr int NR1 = HALF / R1, IT1 = BWT / R1 / 64;
+  static_assert(IT1 >= 1, "the first stage needs every lane");
+  double ca[IT1], sa[IT1], cb[IT1], sb[IT1];
+#pragma unroll
+  for (int it = 0; it < IT1; ++it) {
+    const int j = (lane + 64 * it) % NR1;
+    const d2 p = twd(qt, 2 * j, N), q = twd(qt, 2 * j + 1, N);  // W_N^k = (cos, -sin)(2 pi k / N)
+    ca[it] = p.x;
+    sa[it] = -p.y;
+    cb[it] = q.x;
+    sb[it] = -q.y;
+  }
 #pragma unroll 1
   for (int rd = 0; rd < MSS_TROUNDS; ++rd) {
     const int t0 = blk * PER_WG + (rd * MSS_TW + wave) * FBT;  // this wave's first frame
     if (t0 >= T) break;                                        // wave-uniform
-    // load + window: z_j = w_2j x_2j + i w_2j+1 x_2j+1 (periodic Hann in float64, reflect pad).
-    // All of the batch's samples are loaded before any is used (KT per lane in flight): loads
-    // under the per-element LDS stores were waited for one element at a time (590 us per call).
-    constexpr int KT = FBT * HALF / 64;  // samples pairs per lane: 8 (n <= 1024) or 16 (n = 2048)
-    float xa[KT], xb[KT];
+    // every sample of the batch is loaded before any is used (BWT / 64 pairs per lane in flight)
+    float xa[IT1][R1], xb[IT1][R1];
 #pragma unroll
-    for (int kk = 0; kk < KT; ++kk) {
-      const int e = lane + 64 * kk, u = e / HALF, j = e - u * HALF;
+    for (int it = 0; it < IT1; ++it) {
+      const int idx = lane + 64 * it, u = idx / NR1, j = idx - u * NR1;
       const int t = min(t0 + u, T - 1);
-      const int s0 = t * H + 2 * j - HALF;
-      xa[kk] = x[reflect(s0, L)];
-      xb[kk] = x[reflect(s0 + 1, L)];
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const int s0 = t * H + 2 * (j + r * NR1) - HALF;
+        xa[it][r] = x[reflect(s0, L)];
+        xb[it][r] = x[reflect(s0 + 1, L)];
+      }
     }
 #pragma unroll
-    for (int kk = 0; kk < KT; ++kk) {
-      const int e = lane + 64 * kk, u = e / HALF, j = e - u * HALF;
-      const d2 c0 = twd(qt, 2 * j, N), c1 = twd(qt, 2 * j + 1, N);  // W_N^k: cos(2 pi k / N)
-      const double w0 = 0.5 - 0.5 * c0.x, w1 = 0.5 - 0.5 * c1.x;
-      S[tsw(e)] = dk(w0 * (double)xa[kk], w1 * (double)xb[kk]);
+    for (int it = 0; it < IT1; ++it) {
+      const int idx = lane + 64 * it, u = idx / NR1, j = idx - u * NR1;
+      d2 v[R1];
+#pragma unroll
+      for (int r = 0; r < R1; ++r) {
+        const d2 rot = wturn<R1>(r);  // (cos, -sin)(2 pi r / R1), compile-time
+        const double wa = 0.5 - 0.5 * (ca[it] * rot.x + sa[it] * rot.y);
+        const double wb = 0.5 - 0.5 * (cb[it] * rot.x + sb[it] * rot.y);
+        v[r] = dk(wa * (double)xa[it][r], wb * (double)xb[it][r]);
+      }
+      dft_d<R1>(v);
+      const int pb = tsw(u * HALF + j * R1);
+#pragma unroll
+      for (int r = 0; r < R1; ++r) S[pb ^ tsw(r)] = v[r];
     }
     wave_sync();
-    wave_fft_d<LOG2N - 1, BWT>(S, qt, lane);
+    stages_d<HALF, BWT, R1>(S, qt, lane);
     // post-twist X_f = E + W_N^f O, E = (Z_f + conj Z_(n/2-f)) / 2, O = -i (Z_f - conj Z_(n/2-f)) / 2
 #pragma unroll
     for (int jj = 0; jj < NEO; ++jj) {

@@ -1,8 +1,12 @@
 """Search for an XOR-linear LDS swizzle for the float64 FFT of mss_target_kernel (dev tool).
 
-Models every LDS access of its loads, Stockham stages and post-twist at n = 64 .. 2048 against
-the ds_read_b128 / ds_write_b128 bank rules of MI355X_MICROARCH.md and counts conflict cycles;
-greedy + random-restart local search over swizzles i ^ h(bits 3..10 of i)."""
+Models every LDS access of its Stockham stages and post-twist at n = 64 .. 2048 against the
+ds_read_b128 / ds_write_b128 bank rules of MI355X_MICROARCH.md and counts conflict cycles;
+greedy + random-restart local search over swizzles i ^ h(bits 3..10 of i).
+
+  python tools/lds_swizzle_search.py          # round-5 schedule: load pass + radix-4 stages
+  python tools/lds_swizzle_search.py radix8   # round 6: first stage in registers, then radix 8
+                                              # (remainder 2 / 4; radix 16 first at n = 2048)"""
 import itertools, random
 import numpy as np
 G128R = [list(range(0,4))+list(range(12,16))+list(range(20,28)),
@@ -77,8 +81,36 @@ def mkphys(vecs, size):
     for b, v in vecs.items():
         h ^= ((i >> b) & 1) * v
     return i ^ h
+def sched8(L, BWT):
+    if L == 10 and BWT >= 1024:
+        return [16, 8, 8]
+    a, b = divmod(L, 3)
+    return [8] * a + ([2 ** b] if b else [])
+def patterns_radix8(LOG2M, BWT):
+    """the round-6 schedule: the first stage's inputs come from registers (no load pass)"""
+    N = 1 << LOG2M; acc = []; Ns = 1
+    for si, R in enumerate(sched8(LOG2M, BWT)):
+        NR = N // R; IT = BWT // R // 64
+        if si > 0:
+            for it in range(IT):
+                idx = [l + 64*it for l in range(64)]
+                for r in range(R):
+                    acc.append(('r', [(i//NR)*N + i%NR + r*NR for i in idx]))
+        for it in range(IT):
+            idx = [l + 64*it for l in range(64)]
+            for r in range(R):
+                el = []
+                for i in idx:
+                    fr, j = i//NR, i%NR; k = j % Ns
+                    el.append(fr*N + (j-k)*R + k + r*Ns)
+                acc.append(('w', el))
+        Ns *= R
+    acc += [a for a in patterns(LOG2M, BWT) if a[0] == 'r'][-2 * ((BWT // N * (N + 1) + 63) // 64):]
+    return acc
+import sys
 configs = [(5,512),(6,512),(7,512),(8,512),(9,512),(10,1024)]
-allp = {c: patterns(*c) for c in configs}
+gen = patterns_radix8 if sys.argv[1:] == ['radix8'] else patterns
+allp = {c: gen(*c) for c in configs}
 ident = {c: cost(np.arange(c[1]), allp[c]) for c in configs}
 print("identity", ident, sum(ident.values()))
 best = None
