@@ -83,9 +83,9 @@ __device__ __forceinline__ int reflect(int i, int L) {
 // its RWIN / 256 owned samples (kept in registers) in increasing frame order, so the summation
 // order per sample is the frame order, as in the cooperative kernel above.
 template <bool INV>
-__device__ __forceinline__ c2 twq(const c2* qt, int m, int N) {  // W_N^m from the quarter table
+__device__ __forceinline__ c2 twq(const c2* qt, unsigned m, unsigned N) {  // W_N^m, quarter table
   m &= N - 1;
-  const int Q = N >> 2, q = m / Q, r = m & (Q - 1);
+  const unsigned Q = N >> 2, q = m / Q, r = m & (Q - 1);
   const c2 w = qt[r];
   // times (-i)^q by selects (an if/else chain on the per-lane quadrant compiled to divergent
   // branches around each lookup)
@@ -102,76 +102,104 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// FB = BW / N transforms of size N = 2^LOG2N, in place in s[0 .. BW) (Stockham order per stage:
-// inputs read to registers, then outputs written), natural-order result.
-template <int LOG2N, int BW, bool INV>
-__device__ __forceinline__ void wave_fft(c2* s, const c2* qt, int lane) {
-  constexpr int N = 1 << LOG2N, NR = N / 4, IT = BW / 4 / 64;
-  int Ns = 1;
+// a W_R^k (INV: a W_R^-k) for a compile-time k < R / 2: exact forms for 1, -+i, (1 -+ i) / sqrt 2
+template <int R, bool INV>
+__device__ __forceinline__ c2 wconst_f(c2 a, int k) {
+  if (k == 0) return a;
+  if (4 * k == R) return INV ? mk(-a.y, a.x) : mk(a.y, -a.x);
+  constexpr float h = 0.70710678118654752f;
+  if (8 * k == R) return INV ? mk(h * (a.x - a.y), h * (a.x + a.y)) : mk(h * (a.x + a.y), h * (a.y - a.x));
+  if (8 * k == 3 * R) return INV ? mk(-h * (a.x + a.y), h * (a.x - a.y)) : mk(h * (a.y - a.x), -h * (a.x + a.y));
+  const int m = k * (2048 / R), q = m >> 9;  // W2048^m = (-i)^q W2048^(m mod 512), q < 2
+  const float2 w = kMssW2048.w[m & 511];
+  c2 t = q ? mk(w.y, -w.x) : mk(w.x, w.y);
+  if (INV) t.y = -t.y;
+  return cmul(a, t);
+}
+
+// DFT of R = 2^k points in registers, natural order (radix-2 decimation in time over dft4)
+template <int R, bool INV>
+__device__ __forceinline__ void dft_f(c2 (&v)[R]) {
+  if constexpr (R == 2) {
+    const c2 a = v[0], b = v[1];
+    v[0] = a + b;
+    v[1] = a - b;
+  } else if constexpr (R == 4) {
+    dft4<INV>(v[0], v[1], v[2], v[3]);
+  } else {
+    c2 e[R / 2], o[R / 2];
 #pragma unroll
-  for (int st = 0; st < LOG2N / 2; ++st) {
-    c2 v[IT][4];
-    int ln = lane;
-    __asm__ volatile("" : "+v"(ln));  // lane-derived addresses formed per stage, not kept live
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = ln + 64 * it, fr = idx / NR, j = idx - fr * NR;
-      const c2* src = s + fr * N + j;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[it][r] = src[r * NR];
+    for (int i = 0; i < R / 2; ++i) {
+      e[i] = v[2 * i];
+      o[i] = v[2 * i + 1];
     }
-    wave_sync();
-    const int step = N / (Ns * 4);
+    dft_f<R / 2, INV>(e);
+    dft_f<R / 2, INV>(o);
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = ln + 64 * it, fr = idx / NR, j = idx - fr * NR;
-      const int k = j & (Ns - 1);
-      if (st > 0) {  // k step < N / 4: one quarter-table entry, its square and cube
-        c2 w1 = qt[k * step];
-        if (INV) w1.y = -w1.y;
-        const c2 w2 = cmul(w1, w1);
-        v[it][1] = cmul(v[it][1], w1);
-        v[it][2] = cmul(v[it][2], w2);
-        v[it][3] = cmul(v[it][3], cmul(w2, w1));
-      }
-      dft4<INV>(v[it][0], v[it][1], v[it][2], v[it][3]);
-      c2* d = s + fr * N + (j - k) * 4 + k;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) d[r * Ns] = v[it][r];
+    for (int k = 0; k < R / 2; ++k) {
+      const c2 t = wconst_f<R, INV>(o[k], k);
+      v[k] = e[k] + t;
+      v[k + R / 2] = e[k] - t;
     }
-    wave_sync();
-    Ns *= 4;
   }
-  if constexpr (LOG2N & 1) {
-    constexpr int NR2 = N / 2, IT2 = BW / 2 / 64;
-    c2 v[IT2][2];
-    int ln = lane;
-    __asm__ volatile("" : "+v"(ln));
+}
+
+// One Stockham radix-R stage of the BWP / M transforms of size M in place in s (Ns = product of
+// the earlier radices; qt = the M-point quarter table): every input of the wave is read to
+// registers, then written, so no workgroup barrier sits inside an FFT. The twiddle powers are
+// formed as w^r = w^(r/2) w^(r - r/2) (at most three products deep).
+template <int R, int M, int BWP, int Ns, bool INV>
+__device__ __forceinline__ void stage_f(c2* s, const c2* qt, unsigned lane) {
+  constexpr int NR = M / R, IT = BWP / R / 64;
+  static_assert(IT >= 1, "a stage needs every lane");
+  c2 v[IT][R];
+  unsigned ln = lane;
+  __asm__ volatile("" : "+v"(ln));  // lane-derived addresses formed per stage, not kept live
 #pragma unroll
-    for (int it = 0; it < IT2; ++it) {
-      const int idx = ln + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
-      v[it][0] = s[fr * N + j];
-      v[it][1] = s[fr * N + j + NR2];
-    }
-    wave_sync();
+  for (int it = 0; it < IT; ++it) {
+    const unsigned idx = ln + 64u * it, fr = idx / NR, j = idx % NR;
+    const c2* src = s + fr * M + j;
 #pragma unroll
-    for (int it = 0; it < IT2; ++it) {
-      const int idx = ln + 64 * it, fr = idx / NR2, j = idx - fr * NR2;
-      const int k = j & (Ns - 1);
-      const c2 b = cmul(v[it][1], twq<INV>(qt, k, 2 * Ns));
-      c2* d = s + fr * N + (j - k) * 2 + k;
-      d[0] = v[it][0] + b;
-      d[Ns] = v[it][0] - b;
+    for (int r = 0; r < R; ++r) v[it][r] = src[r * NR];
+  }
+  wave_sync();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const unsigned idx = ln + 64u * it, fr = idx / NR, j = idx % NR, k = j & (Ns - 1);
+    if constexpr (Ns > 1) {
+      c2 w[R];
+      w[1] = twq<INV>(qt, k * (M / (R * Ns)), M);
+#pragma unroll
+      for (int r = 2; r < R; ++r) w[r] = cmul(w[r / 2], w[r - r / 2]);
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[it][r] = cmul(v[it][r], w[r]);
     }
-    wave_sync();
+    dft_f<R, INV>(v[it]);
+    c2* d = s + fr * M + (j - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[r * Ns] = v[it][r];
+  }
+  wave_sync();
+}
+
+// the stages from Ns on: radix 8 while 8 divides what is left, then the remainder (2 or 4)
+template <int M, int BWP, int Ns, bool INV>
+__device__ __forceinline__ void stages_f(c2* s, const c2* qt, unsigned lane) {
+  if constexpr (Ns < M) {
+    constexpr int R = M / Ns < 8 ? M / Ns : 8;
+    stage_f<R, M, BWP, Ns, INV>(s, qt, lane);
+    stages_f<M, BWP, Ns * R, INV>(s, qt, lane);
   }
 }
 
 #ifndef MST_MSS_BW
 #define MST_MSS_BW 1024  // complex per wave buffer for n <= MST_MSS_BW (A/B: 512 halves LDS and registers)
 #endif
+#ifndef MSS_REG_FIRST
+#define MSS_REG_FIRST 128  // n/2 from which the forward transform's first stage runs in registers
+#endif
 #ifndef MST_MSS_OCC
-#define MST_MSS_OCC 4
+#define MST_MSS_OCC 4  // mss_multi_kernel workgroups per CU (launch bound; LDS allows 4)
 #endif
 constexpr int MSS_W = 4;  // waves per workgroup
 template <int LOG2N>
@@ -248,56 +276,87 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
         float stv[NE];
 #pragma unroll
         for (int jj = 0; jj < NE; ++jj) {
-          const int e = min(lane + 64 * jj, FB * NBIN - 1), m = e / NBIN, f = e - m * NBIN;
-          const int t = min(t_base + 2 * m + pass, f_own1 - 1);  // clamped: masked below
+          const unsigned e = min(lane + 64u * jj, (unsigned)(FB * NBIN - 1)), m = e / NBIN, f = e % NBIN;
+          const int t = min(t_base + 2 * (int)m + pass, f_own1 - 1);  // clamped: masked below
           stv[jj] = tm[(long long)t * NBIN + f];
         }
         // load + window FB pred frames t_base + 2m + pass, each an n/2-point complex transform
-        // z_j = w_2j x_2j + i w_2j+1 x_2j+1 in the first half of the wave's buffer.
-        // Branch-free: a frame past f_own1 loads frame f_own1 - 1 (always in range) and is
-        // zeroed by a select; a load under a per-element branch made hipcc wait for each
-        // element's loads at the join (32 serialised global round trips per round).
-        constexpr int KC = LOG2N >= 10 ? 4 : 8;  // elements per load batch (2 KC loads in flight)
+        // of z_j = w_2j x_2j + i w_2j+1 x_2j+1. Branch-free: a frame past f_own1 loads frame
+        // f_own1 - 1 (always in range) and is zeroed by a select; a load under a per-element
+        // branch made hipcc wait for each element's loads at the join.
+        if constexpr (HALF >= MSS_REG_FIRST) {
+          // n >= 256: the first radix-R1 stage runs in registers on the loaded samples (lane
+          // element (u, j) takes c = j + r NR1, r < R1) and stores its outputs to the first half
+          // of the wave's buffer. Below that, NR1 consecutive pairs per frame are under 128 B and
+          // the loads' coalescing cost more than the LDS pass saves (n = 64 / 128 ran 3-6 %
+          // slower this way).
+          constexpr int R1 = 8, NR1 = HALF / R1, IT1 = BW / 2 / R1 / 64;
+          static_assert(IT1 >= 1, "the first stage needs every lane");
 #pragma unroll
-        for (int k0 = 0; k0 < BW / 128; k0 += KC) {
-          float x0[KC], x1[KC];
+          for (int it = 0; it < IT1; ++it) {
+            const unsigned idx = lane + 64u * it, u = idx / NR1, j = idx % NR1;
+            const int t = min(t_base + 2 * (int)u + pass, f_own1 - 1);
+            const bool live = t_base + 2 * (int)u + pass < f_own1;
+            float x0[R1], x1[R1];
 #pragma unroll
-          for (int kk = 0; kk < KC; ++kk) {
-            const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
-            const int t = min(t_base + 2 * u + pass, f_own1 - 1);
-            const int s0 = t * H + 2 * j - HALF;
-            x0[kk] = p[reflect(s0, L)];
-            x1[kk] = p[reflect(s0 + 1, L)];
+            for (int r = 0; r < R1; ++r) {
+              const int s0 = t * H + 2 * (int)(j + r * NR1) - HALF;
+              x0[r] = p[reflect(s0, L)];
+              x1[r] = p[reflect(s0 + 1, L)];
+            }
+            c2 v[R1];
+#pragma unroll
+            for (int r = 0; r < R1; ++r) {
+              const float2 wj = *reinterpret_cast<const float2*>(hw + 2 * (j + r * NR1));
+              v[r] = live ? mk(wj.x * x0[r], wj.y * x1[r]) : mk(0.f, 0.f);
+            }
+            dft_f<R1, false>(v);
+            c2* d = S + u * HALF + j * R1;
+#pragma unroll
+            for (int r = 0; r < R1; ++r) d[r] = v[r];
           }
+          wave_sync();
+          stages_f<HALF, BW / 2, R1, false>(S, qth, lane);
+        } else {
+          constexpr int KC = 8;  // elements per load batch (2 KC loads in flight)
 #pragma unroll
-          for (int kk = 0; kk < KC; ++kk) {
-            const int e = lane + 64 * (k0 + kk), u = e / HALF, j = e - u * HALF;
-            const bool live = t_base + 2 * u + pass < f_own1;
-            const float2 wj = *reinterpret_cast<const float2*>(hw + 2 * j);
-            S[e] = live ? mk(wj.x * x0[kk], wj.y * x1[kk]) : mk(0.f, 0.f);
+          for (int k0 = 0; k0 < BW / 128; k0 += KC) {
+            float x0[KC], x1[KC];
+#pragma unroll
+            for (int kk = 0; kk < KC; ++kk) {
+              const unsigned e = lane + 64u * (k0 + kk), u = e / HALF, j = e % HALF;
+              const int t = min(t_base + 2 * (int)u + pass, f_own1 - 1);
+              const int s0 = t * H + 2 * (int)j - HALF;
+              x0[kk] = p[reflect(s0, L)];
+              x1[kk] = p[reflect(s0 + 1, L)];
+            }
+#pragma unroll
+            for (int kk = 0; kk < KC; ++kk) {
+              const unsigned e = lane + 64u * (k0 + kk), u = e / HALF, j = e % HALF;
+              const bool live = t_base + 2 * (int)u + pass < f_own1;
+              const float2 wj = *reinterpret_cast<const float2*>(hw + 2 * j);
+              S[e] = live ? mk(wj.x * x0[kk], wj.y * x1[kk]) : mk(0.f, 0.f);
+            }
           }
+          wave_sync();
+          stages_f<HALF, BW / 2, 1, false>(S, qth, lane);
         }
-        wave_sync();
-        wave_fft<LOG2N - 1, BW / 2, false>(S, qth, lane);
         // spectra, loss, gradient spectra (registers)
 #pragma unroll
         for (int jj = 0; jj < NE; ++jj) {
-          int ln = lane;
+          unsigned ln = lane;
           __asm__ volatile("" : "+v"(ln));  // per-entry indices, not kept live across the loop
-          const int e = ln + 64 * jj, m = e / NBIN, f = e - m * NBIN;
-          const int t = t_base + 2 * m + pass;
+          const unsigned e = ln + 64u * jj, m = e / NBIN, f = e % NBIN;
+          const int t = t_base + 2 * (int)m + pass;
           c2 zg = mk(0.f, 0.f);
           if (e < FB * NBIN && t < f_own1) {
             // real-FFT post-twist of each signal: X_f = E + W_n^f O, E = (Z_f + conj Z_(n/2-f)) / 2,
             // O = -i (Z_f - conj Z_(n/2-f)) / 2, indices mod n/2
             const c2 wf = twq<false>(qt, f, N);
-            const int fa = f & (HALF - 1), fb = (HALF - f) & (HALF - 1);
-            auto bin = [&](const c2* Z) __attribute__((always_inline)) {
-              const c2 A = Z[fa], Bc = conjc(Z[fb]);
-              const c2 E = (A + Bc) * 0.5f, D = A - Bc;
-              return E + cmul(wf, mk(D.y * 0.5f, -D.x * 0.5f));
-            };
-            const c2 P = bin(S + m * HALF);
+            const unsigned fa = f & (HALF - 1), fb = (HALF - f) & (HALF - 1);
+            const c2 A = S[m * HALF + fa], Bc = conjc(S[m * HALF + fb]);
+            const c2 E = (A + Bc) * 0.5f, D = A - Bc;
+            const c2 P = E + cmul(wf, mk(D.y * 0.5f, -D.x * 0.5f));
             // hardware sqrt / log2 / rcp (1 ulp): the library forms add ~10 instructions each
             const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
             const float st = stv[jj];
@@ -322,22 +381,21 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
         // C = H^a + i H^b per pair (H^a_f = Za/2, H^a_{n-f} = conj(Za)/2)
 #pragma unroll
         for (int jj = 0; jj < NE; ++jj) {
-          int ln = lane;
+          unsigned ln = lane;
           __asm__ volatile("" : "+v"(ln));
-          const int e = ln + 64 * jj, m = e / NBIN, f = e - m * NBIN;
+          const unsigned e = ln + 64u * jj, m = e / NBIN, f = e % NBIN;
           if (e < FB * NBIN) {
             const c2 za = zga[jj], zb = zgb[jj];
-            c2* c = S + m * N;
             if (f == 0 || f == HALF) {
-              c[f] = mk(za.x, zb.x);
+              S[m * N + f] = mk(za.x, zb.x);
             } else {
-              c[f] = mk(0.5f * (za.x - zb.y), 0.5f * (za.y + zb.x));
-              c[N - f] = mk(0.5f * (za.x + zb.y), 0.5f * (-za.y + zb.x));
+              S[m * N + f] = mk(0.5f * (za.x - zb.y), 0.5f * (za.y + zb.x));
+              S[m * N + N - f] = mk(0.5f * (za.x + zb.y), 0.5f * (-za.y + zb.x));
             }
           }
         }
         wave_sync();
-        wave_fft<LOG2N, BW, true>(S, qt, lane);
+        stages_f<N, BW, 1, true>(S, qt, lane);
       }
     }
     if (!grad) continue;  // uniform over the workgroup: no barrier needed
@@ -685,7 +743,7 @@ struct MssMulti {
   int nsz;
 };
 
-__global__ __launch_bounds__(256, 4) void mss_multi_kernel(const MssMulti m) {
+__global__ __launch_bounds__(256, MST_MSS_OCC) void mss_multi_kernel(const MssMulti m) {
   __shared__ __attribute__((aligned(16))) char lds[MSS_LDS_MAX];
   const int z = blockIdx.z;
   const MssArgs& a = m.s[z];
