@@ -1684,17 +1684,15 @@ __device__ __forceinline__ int mss_reflect(int i, int L) {
 // z[n] = g[2n] + i g[2n+1] = IDFT1024(Z'), Z'_k = A + i e^(i pi k / 1024) B with
 // A = Y_k + conj Y_(1024-k), B = Y_k - conj Y_(1024-k); Z'_(1024-k) = conj A + i conj(e B) goes to
 // lane 64 - l, register 15 - j (lane 0 keeps its own). Frames a and b of a pair then sit in the
-// wave's LDS buffer as (g_a, g_b) for the workgroup's ordered overlap-add. Three fft1024_v2 per
-// frame, as in the packed form this replaces.
-__device__ __forceinline__ c2 mss_term(c2 P, float st, bool use, bool own, bool grad, const MssArgs& a,
+// wave's LDS buffer as (g_a, g_b) for the workgroup's ordered overlap-add. Two fft1024_v2 per
+// frame (the target's magnitudes come from mss_target2048_kernel).
+__device__ __forceinline__ c2 mss_term(c2 P, float st, bool use, bool grad, const MssArgs& a,
                                        float& s_abs, float& s_log) {
   const float sp = __builtin_amdgcn_sqrtf(P.x * P.x + P.y * P.y);
   c2 g2 = mk(0.f, 0.f);
   if (use) {
-    if (own) {
-      s_abs += fabsf(sp - st);
-      s_log += fabsf(__log2f(sp + a.eps) * 0.69314718055994531f - __log2f(st + a.eps) * 0.69314718055994531f);
-    }
+    s_abs += fabsf(sp - st);
+    s_log += fabsf(__log2f(sp + a.eps) * 0.69314718055994531f - __log2f(st + a.eps) * 0.69314718055994531f);
     if (grad && sp > 0.f) {
       const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
       const float g = sg * (1.f + a.alpha * __builtin_amdgcn_rcpf(sp + a.eps)) * a.inv_cnt;
@@ -1725,6 +1723,7 @@ __device__ __forceinline__ void real_pairs(const c2 v[16], const FftTabs& tb, in
 
 __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   constexpr int N = 2048, H = N / 4, HALF = N / 2, W = 4, OWN = MSS_RWIN / 256;
+  constexpr int SPILL = 3 * H / 256;  // per thread: samples past the range its frames reach
   __shared__ __attribute__((aligned(16))) c2 buf[W * N];  // per wave: FFT scratch, then G
   __shared__ __attribute__((aligned(16))) FftTabs tb;
   __shared__ float red[2][W];
@@ -1748,11 +1747,13 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   };
   const int own_lo = w * MSS_RWIN;
   const int f_own0 = w * (MSS_RWIN / H), f_own1 = min(f_own0 + MSS_RWIN / H, a.T);
-  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
+  // frames [f_own0, f_own1) only (one round): the gradient of the last three on the 3H samples
+  // past the range goes to a.spill (mss_spill_kernel, mss.hip), as in mss_wave_body
+  const int f_lo = f_own0;
   c2* S = buf + wave * N;
-  float acc[OWN];
+  float acc[OWN + SPILL];  // sample own_lo + tid + 256 i (i >= OWN: past the range)
 #pragma unroll
-  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
+  for (int i = 0; i < OWN + SPILL; ++i) acc[i] = 0.f;
   float s_abs = 0.f, s_log = 0.f;
 
 #pragma unroll 1
@@ -1791,17 +1792,16 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
           }
         }
         fft1024_v2(vp, S, tb, lane);  // Z_pred[l + 64 j]
-        const bool own = t >= f_own0;
         c2 pk[8], pm[8], yk[8], ym[8];
         real_pairs(vp, tb, lane, src, pk, pm);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          yk[j] = mss_term(pk[j], qk[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
+          yk[j] = mss_term(pk[j], qk[j], valid, grad, a, s_abs, s_log) * 0.5f;
           // lane 0's X[1024 - 0] is the Nyquist bin X[1024] (xm[0]), its magnitude tr[1024]
-          ym[j] = mss_term(pm[j], qm[j], valid, own, grad, a, s_abs, s_log) * 0.5f;
+          ym[j] = mss_term(pm[j], qm[j], valid, grad, a, s_abs, s_log) * 0.5f;
         }
         // f = 512: X[512] = conj Z[512] (lane 0, register 8)
-        const c2 y512 = mss_term(conj(vp[8]), q512, valid && lane == 0, own, grad, a, s_abs, s_log) * 0.5f;
+        const c2 y512 = mss_term(conj(vp[8]), q512, valid && lane == 0, grad, a, s_abs, s_log) * 0.5f;
         if (!grad) continue;
         if (lane == 0) {  // Y_0, Y_1024 are real (and G_f / 2 -> G_f there)
           yk[0] = mk(2.f * yk[0].x, 0.f);
@@ -1845,7 +1845,7 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
     __syncthreads();
     const int r_hi = min(t_round + 2 * W, f_own1);
 #pragma unroll
-    for (int i = 0; i < OWN; ++i) {
+    for (int i = 0; i < OWN + SPILL; ++i) {
       const int sp = own_lo + tid + 256 * i;
       const int th = sp / H;
       const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
@@ -1891,6 +1891,9 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
     float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
     if (pp < own_hi) *dst = acc[i];
   }
+  float* spl = a.spill + ((long long)b * a.nwg + w) * (3 * H);
+#pragma unroll
+  for (int i = 0; i < SPILL; ++i) spl[tid + 256 * i] = acc[OWN + i];
 }
 
 }  // namespace

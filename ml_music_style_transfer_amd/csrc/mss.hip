@@ -222,6 +222,7 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
   constexpr int RF = W * GF;                 // frames per round
   constexpr int NE = (FB * NBIN + 63) / 64;  // spectrum entries per lane
   constexpr int OWN = RWIN / 256;            // owned samples per thread
+  constexpr int SPILL = (3 * H + 255) / 256;  // per thread: samples past the range its frames reach
   c2* buf = reinterpret_cast<c2*>(lds);                                   // [W * BW]
   c2* qt = buf + W * BW;                                                  // [N / 4]
   c2* qth = qt + N / 4;  // quarter table of the n/2-point forward transforms  [N / 8]
@@ -256,11 +257,14 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
 
   const int own_lo = w * RWIN;
   const int f_own0 = w * (RWIN / H), f_own1 = min(f_own0 + RWIN / H, a.T);
-  const int f_lo = grad ? max(f_own0 - 3, 0) : f_own0;
+  // Frames [f_own0, f_own1) only: the last three reach 3H samples into the next workgroup's
+  // range, and those sums go to a.spill for mss_spill_kernel to add there (round 5 recomputed the
+  // previous range's last three frames here instead: a nearly empty third round per workgroup).
+  const int f_lo = f_own0;
   c2* S = buf + wave * BW;
-  float acc[OWN];
+  float acc[OWN + SPILL];  // sample own_lo + tid + 256 i (i >= OWN: past the range)
 #pragma unroll
-  for (int i = 0; i < OWN; ++i) acc[i] = 0.f;
+  for (int i = 0; i < OWN + SPILL; ++i) acc[i] = 0.f;
   float s_abs = 0.f, s_log = 0.f;
 
 #pragma unroll 1
@@ -362,10 +366,8 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
             const float st = stv[jj];
             const float lp = __log2f(sp + a.eps) * 0.69314718055994531f;
             const float lt = __log2f(st + a.eps) * 0.69314718055994531f;
-            if (t >= f_own0) {
-              s_abs += fabsf(sp - st);
-              s_log += fabsf(lp - lt);
-            }
+            s_abs += fabsf(sp - st);
+            s_log += fabsf(lp - lt);
             if (grad && sp > 0.f) {
               const float sg = sp > st ? 1.f : (sp < st ? -1.f : 0.f);
               const float g = sg * (1.f + a.alpha * __builtin_amdgcn_rcpf(sp + a.eps)) * a.inv_cnt;
@@ -403,7 +405,7 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
     // windowed overlap-add of the round's frames into the owned samples, frames in order
     const int r_hi = min(t_round + RF, f_own1);
 #pragma unroll
-    for (int i = 0; i < OWN; ++i) {
+    for (int i = 0; i < OWN + SPILL; ++i) {
       const int sp = own_lo + tid + 256 * i;  // padded coordinate
       const int th = sp / H;
       const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
@@ -448,6 +450,12 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
     const int x = pp - HALF;
     float* dst = x < 0 ? ed + pp : (x >= L ? ed + HALF + (x - L) : dp + x);
     if (pp < own_hi) *dst = acc[i];
+  }
+  float* spl = a.spill + ((long long)b * a.nwg + w) * (3 * H);
+#pragma unroll
+  for (int i = 0; i < SPILL; ++i) {
+    const int o = tid + 256 * i;
+    if (o < 3 * H) spl[o] = acc[OWN + i];
   }
 }
 
@@ -758,6 +766,33 @@ __global__ __launch_bounds__(256, MST_MSS_OCC) void mss_multi_kernel(const MssMu
   }
 }
 
+// Adds the gradient a workgroup's last three frames put past its range (a.spill, 3n/4 padded
+// samples) to the next workgroup's first samples in the size's slab (or its tail-pad edge
+// gradient); each destination gets exactly one add. Grid (ceil(3 n_max / 4 / 256) x B,
+// nwg_max - 1, sizes); destination w (>= 1) takes source w - 1.
+struct SpillArgs {
+  float* slab[8];
+  float* edges[8];
+  const float* spill[8];
+  long long L;
+  int nsz, gx;
+  int n[8], nwg[8];
+};
+
+__global__ __launch_bounds__(256) void mss_spill_kernel(const SpillArgs a) {
+  const int s = blockIdx.z, b = blockIdx.x / a.gx, w = blockIdx.y + 1;
+  const int n = a.n[s], half = n / 2, hs = 3 * n / 4;
+  const int o = (blockIdx.x - b * a.gx) * 256 + threadIdx.x;
+  const long long L = a.L;
+  if (w >= a.nwg[s] || o >= hs) return;
+  const long long pp = (long long)w * MSS_RWIN + o;  // padded coordinate (>= MSS_RWIN > n / 2)
+  if (pp >= L + n) return;
+  const float v = a.spill[s][((long long)b * a.nwg[s] + w - 1) * hs + o];
+  const long long x = pp - half;
+  float* dst = x >= L ? a.edges[s] + (long long)b * n + half + (x - L) : a.slab[s] + b * L + x;
+  *dst += v;
+}
+
 // dpred[i] = ((slab_0 + slab_1) + ...) [i], the sizes in call order (the per-size launches' order);
 // slabs are `stride` floats apart (a multiple of 4, 16-byte aligned); vec: dpred 16-byte aligned
 __global__ __launch_bounds__(256) void mss_sum_kernel(const float* __restrict__ slabs, long long n,
@@ -886,7 +921,7 @@ int log2i(int n) {
 struct Plan {
   int nsz;
   int n[8], T[8], nwg[8];
-  long long part_off[8], edge_off[8], slab_off[8], slab_stride, tmag_off[8];
+  long long part_off[8], edge_off[8], slab_off[8], slab_stride, tmag_off[8], spill_off[8];
   size_t bytes;
 };
 
@@ -915,6 +950,11 @@ int make_plan(int64_t B, int64_t L, int32_t n_sizes, const int32_t* sizes, Plan&
   for (int s = 0; s < n_sizes; ++s) {
     pl.tmag_off[s] = tm;
     tm += (B * pl.T[s] * (pl.n[s] / 2 + 1) + 3) / 4 * 4;
+  }
+  // the gradient past each workgroup's range per size (B, nwg, 3n/4)
+  for (int s = 0; s < n_sizes; ++s) {
+    pl.spill_off[s] = tm;
+    tm += B * pl.nwg[s] * (3 * pl.n[s] / 4);
   }
   pl.bytes = (size_t)tm * sizeof(float);
   for (int s = 0; s < n_sizes; ++s) pl.edge_off[s] += part;
@@ -982,6 +1022,7 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     a.dpred = dpred ? w + pl.slab_off[s] : nullptr;  // this size's slab
     a.edges = w + pl.edge_off[s];
     a.partial = w + pl.part_off[s];
+    a.spill = w + pl.spill_off[s];
     const int lg = log2i(pl.n[s]);
     if (lg == 11) {  // register-resident fft1024_v2 kernel (fft.hip)
       mss_fft2048_launch(a, (unsigned)pl.nwg[s], (unsigned)B, st);
@@ -996,6 +1037,26 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
   if (mm.nsz > 0) {
     hipLaunchKernelGGL(mss_multi_kernel, dim3(max_nwg, (unsigned)B, (unsigned)mm.nsz), dim3(256), 0, st, mm);
     MST_CHECK_LAUNCH();
+  }
+  if (dpred) {
+    SpillArgs sa;
+    sa.L = L;
+    sa.nsz = pl.nsz;
+    unsigned gx = 0, gy = 0;
+    for (int s = 0; s < pl.nsz; ++s) {
+      sa.slab[s] = w + pl.slab_off[s];
+      sa.edges[s] = w + pl.edge_off[s];
+      sa.spill[s] = w + pl.spill_off[s];
+      sa.n[s] = pl.n[s];
+      sa.nwg[s] = pl.nwg[s];
+      gx = max(gx, (unsigned)ceil_div(3 * pl.n[s] / 4, 256));
+      gy = max(gy, (unsigned)(pl.nwg[s] - 1));
+    }
+    sa.gx = (int)gx;
+    if (gy > 0) {
+      hipLaunchKernelGGL(mss_spill_kernel, dim3(gx * (unsigned)B, gy, (unsigned)pl.nsz), dim3(256), 0, st, sa);
+      MST_CHECK_LAUNCH();
+    }
   }
   if (dpred) {
     const long long n = B * L;
