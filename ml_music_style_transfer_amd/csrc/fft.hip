@@ -1748,7 +1748,7 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
   const int own_lo = w * MSS_RWIN;
   const int f_own0 = w * (MSS_RWIN / H), f_own1 = min(f_own0 + MSS_RWIN / H, a.T);
   // frames [f_own0, f_own1) only (one round): the gradient of the last three on the 3H samples
-  // past the range goes to a.spill (mss_spill_kernel, mss.hip), as in mss_wave_body
+  // past the range goes to a.spill (added by mss_sum_kernel / mss_fold, mss.hip), as in mss_wave_body
   const int f_lo = f_own0;
   c2* S = buf + wave * N;
   float acc[OWN + SPILL];  // sample own_lo + tid + 256 i (i >= OWN: past the range)

@@ -9,15 +9,17 @@
 //
 // Sizes n = 64 .. 1024 run in ONE launch (mss_multi_kernel, grid z = size) and n = 2048 in
 // mss_fft2048_kernel (fft.hip). A workgroup owns R = 4096 consecutive samples of one clip's padded
-// signal and computes every frame that overlaps them (3 halo frames recomputed at the left
-// edge), so the gradient is accumulated on chip and written once: no atomics, no spectra in
-// HBM. Every frame of pred and of target is transformed on its own as a real FFT (an n/2-point
+// signal and the frames starting in them, so the gradient is accumulated on chip and written
+// once: no atomics, no spectra in HBM. Every frame of pred and of target is transformed on its own as a real FFT (an n/2-point
 // complex transform of the even/odd samples plus the post-twist), in place inside one wave;
 // the two gradient frames of a frame pair are packed into one Hermitian-completed inverse
 // transform (real part = frame a, imaginary part = frame b). The target is transformed once per
 // call, in float64 (mss_target_kernel), and the loss kernels read its magnitudes.
-// Deterministic: fixed summation order everywhere; each size writes its own gradient slab and
-// mss_sum_kernel adds the slabs in size order; reflect-pad edges are folded in by a final kernel.
+// The gradient a workgroup's last three frames put on the 3n/4 samples past its range goes to a
+// spill slab (round 5 recomputed those three frames in the next workgroup instead).
+// Deterministic: fixed summation order everywhere; each size writes its own gradient and spill
+// slabs and mss_sum_kernel adds them in size order; reflect-pad edges are folded in by a final
+// kernel.
 #include <cstdlib>
 
 #include "common.h"
@@ -258,7 +260,7 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
   const int own_lo = w * RWIN;
   const int f_own0 = w * (RWIN / H), f_own1 = min(f_own0 + RWIN / H, a.T);
   // Frames [f_own0, f_own1) only: the last three reach 3H samples into the next workgroup's
-  // range, and those sums go to a.spill for mss_spill_kernel to add there (round 5 recomputed the
+  // range, and those sums go to a.spill for mss_sum_kernel / mss_fold to add (round 5 recomputed the
   // previous range's last three frames here instead: a nearly empty third round per workgroup).
   const int f_lo = f_own0;
   c2* S = buf + wave * BW;
@@ -766,51 +768,54 @@ __global__ __launch_bounds__(256, MST_MSS_OCC) void mss_multi_kernel(const MssMu
   }
 }
 
-// Adds the gradient a workgroup's last three frames put past its range (a.spill, 3n/4 padded
-// samples) to the next workgroup's first samples in the size's slab (or its tail-pad edge
-// gradient); each destination gets exactly one add. Grid (ceil(3 n_max / 4 / 256) x B,
-// nwg_max - 1, sizes); destination w (>= 1) takes source w - 1.
-struct SpillArgs {
-  float* slab[8];
-  float* edges[8];
-  const float* spill[8];
-  long long L;
-  int nsz, gx;
-  int n[8], nwg[8];
-};
-
-__global__ __launch_bounds__(256) void mss_spill_kernel(const SpillArgs a) {
-  const int s = blockIdx.z, b = blockIdx.x / a.gx, w = blockIdx.y + 1;
-  const int n = a.n[s], half = n / 2, hs = 3 * n / 4;
-  const int o = (blockIdx.x - b * a.gx) * 256 + threadIdx.x;
-  const long long L = a.L;
-  if (w >= a.nwg[s] || o >= hs) return;
-  const long long pp = (long long)w * MSS_RWIN + o;  // padded coordinate (>= MSS_RWIN > n / 2)
-  if (pp >= L + n) return;
-  const float v = a.spill[s][((long long)b * a.nwg[s] + w - 1) * hs + o];
-  const long long x = pp - half;
-  float* dst = x >= L ? a.edges[s] + (long long)b * n + half + (x - L) : a.slab[s] + b * L + x;
-  *dst += v;
+// The gradient a workgroup's last three frames put on the 3n/4 padded samples past its range
+// (MssArgs::spill): the value for padded sample pp of clip b, or 0 where no workgroup spills.
+__device__ __forceinline__ float spill_at(const float* sp, int nwg, int hs, long long b, long long pp) {
+  const long long w = pp / MSS_RWIN;
+  const int o = (int)(pp - w * MSS_RWIN);
+  return (w >= 1 && w < nwg && o < hs) ? sp[(b * nwg + w - 1) * hs + o] : 0.f;
 }
 
-// dpred[i] = ((slab_0 + slab_1) + ...) [i], the sizes in call order (the per-size launches' order);
-// slabs are `stride` floats apart (a multiple of 4, 16-byte aligned); vec: dpred 16-byte aligned
-__global__ __launch_bounds__(256) void mss_sum_kernel(const float* __restrict__ slabs, long long n,
-                                                      long long stride, int nsz, int vec,
-                                                      float* __restrict__ dpred) {
-  const long long n4 = vec ? n >> 2 : 0;
-  const f32x4* sl = reinterpret_cast<const f32x4*>(slabs);
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    f32x4 v = sl[i];
-    for (int s = 1; s < nsz; ++s) v += sl[s * (stride >> 2) + i];
-    reinterpret_cast<f32x4*>(dpred)[i] = v;
+// dpred[b, x] = sum over sizes in call order (the per-size launches' order) of that size's slab
+// plus the spill from the previous workgroup's range (spill_at). Grid (blocks, B): one clip row
+// per blockIdx.y. vec: L % 4 == 0 and dpred 16-byte aligned (the slabs are, stride a multiple of
+// 4); a 4-sample group never straddles a spill boundary (MSS_RWIN, n / 2 and 3n / 4 are multiples
+// of 4).
+struct SumArgs {
+  const float* slabs;  // size s's slab at slabs + s * stride, (B, L) each
+  long long stride, L;
+  int nsz, vec;
+  float* dpred;
+  const float* spill[8];
+  int half[8], hs[8], nwg[8];
+};
+
+__global__ __launch_bounds__(256) void mss_sum_kernel(const SumArgs a) {
+  const long long b = blockIdx.y, L = a.L;
+  float* dp = a.dpred + b * L;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  if (a.vec) {
+    for (long long x = 4 * ((long long)blockIdx.x * blockDim.x + threadIdx.x); x < L; x += 4 * step) {
+      f32x4 v;
+      for (int s = 0; s < a.nsz; ++s) {
+        f32x4 t = *reinterpret_cast<const f32x4*>(a.slabs + s * a.stride + b * L + x);
+        const long long pp = x + a.half[s], w = pp / MSS_RWIN;
+        const int o = (int)(pp - w * MSS_RWIN);
+        if (w >= 1 && w < a.nwg[s] && o < a.hs[s])
+          t += *reinterpret_cast<const f32x4*>(a.spill[s] + (b * a.nwg[s] + w - 1) * a.hs[s] + o);
+        v = s == 0 ? t : v + t;
+      }
+      *reinterpret_cast<f32x4*>(dp + x) = v;
+    }
+    return;
   }
-  for (long long i = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float v = slabs[i];
-    for (int s = 1; s < nsz; ++s) v += slabs[s * stride + i];
-    dpred[i] = v;
+  for (long long x = (long long)blockIdx.x * blockDim.x + threadIdx.x; x < L; x += step) {
+    float v = 0.f;
+    for (int s = 0; s < a.nsz; ++s) {
+      const float t = a.slabs[s * a.stride + b * L + x] + spill_at(a.spill[s], a.nwg[s], a.hs[s], b, x + a.half[s]);
+      v = s == 0 ? t : v + t;
+    }
+    dp[x] = v;
   }
 }
 
@@ -822,6 +827,8 @@ struct FoldArgs {
   int B, nsz;
   int n[8];
   long long off[8];
+  const float* spill[8];  // the tail-pad samples' spill (spill_at), by size
+  int nwg[8];
 };
 
 __device__ void mss_fold(const FoldArgs& a, int b) {
@@ -840,7 +847,7 @@ __device__ void mss_fold(const FoldArgs& a, int b) {
         const int half = a.n[s] / 2;
         const float* ed = a.edges + a.off[s] + (long long)b * a.n[s];
         if (h <= half) vh += ed[half - h];
-        if (i < half) vt += ed[half + i];
+        if (i < half) vt += ed[half + i] + spill_at(a.spill[s], a.nwg[s], 3 * a.n[s] / 4, b, a.L + half + i);
       }
       dp[h] = vh;
       dp[L - 2 - i] = vt;
@@ -852,7 +859,8 @@ __device__ void mss_fold(const FoldArgs& a, int b) {
     const float* ed = a.edges + a.off[s] + (long long)b * n;
     for (int k = threadIdx.x; k < half; k += blockDim.x) dp[half - k] += ed[k];
     __syncthreads();
-    for (int k = threadIdx.x; k < half; k += blockDim.x) dp[L - 2 - k] += ed[half + k];
+    for (int k = threadIdx.x; k < half; k += blockDim.x)
+      dp[L - 2 - k] += ed[half + k] + spill_at(a.spill[s], a.nwg[s], 3 * n / 4, b, a.L + half + k);
     __syncthreads();
   }
 }
@@ -1039,31 +1047,22 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
     MST_CHECK_LAUNCH();
   }
   if (dpred) {
-    SpillArgs sa;
+    SumArgs sa;
+    sa.slabs = w + pl.slab_off[0];
+    sa.stride = pl.slab_stride;
     sa.L = L;
     sa.nsz = pl.nsz;
-    unsigned gx = 0, gy = 0;
+    sa.vec = (L % 4 == 0 && ((uintptr_t)dpred & 15) == 0) ? 1 : 0;
+    sa.dpred = dpred;
     for (int s = 0; s < pl.nsz; ++s) {
-      sa.slab[s] = w + pl.slab_off[s];
-      sa.edges[s] = w + pl.edge_off[s];
       sa.spill[s] = w + pl.spill_off[s];
-      sa.n[s] = pl.n[s];
+      sa.half[s] = pl.n[s] / 2;
+      sa.hs[s] = 3 * pl.n[s] / 4;
       sa.nwg[s] = pl.nwg[s];
-      gx = max(gx, (unsigned)ceil_div(3 * pl.n[s] / 4, 256));
-      gy = max(gy, (unsigned)(pl.nwg[s] - 1));
     }
-    sa.gx = (int)gx;
-    if (gy > 0) {
-      hipLaunchKernelGGL(mss_spill_kernel, dim3(gx * (unsigned)B, gy, (unsigned)pl.nsz), dim3(256), 0, st, sa);
-      MST_CHECK_LAUNCH();
-    }
-  }
-  if (dpred) {
-    const long long n = B * L;
-    const long long blocks = (n / 4 + 256) / 256;
-    hipLaunchKernelGGL(mss_sum_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, st,
-                       (const float*)(w + pl.slab_off[0]), n, pl.slab_stride, pl.nsz,
-                       ((uintptr_t)dpred & 15) == 0 ? 1 : 0, dpred);
+    const long long per = sa.vec ? (L + 3) / 4 : L;
+    const long long blocks = (per + 255) / 256;
+    hipLaunchKernelGGL(mss_sum_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024), (unsigned)B), dim3(256), 0, st, sa);
     MST_CHECK_LAUNCH();
   }
   FinishArgs fa;
@@ -1082,6 +1081,8 @@ int mst_mss_loss_f32(const float* pred, const float* target, int64_t B, int64_t 
   for (int s = 0; s < pl.nsz; ++s) {
     f.n[s] = pl.n[s];
     f.off[s] = pl.edge_off[s];
+    f.spill[s] = w + pl.spill_off[s];
+    f.nwg[s] = pl.nwg[s];
     la.off[s] = pl.part_off[s];
     la.cnt[s] = (int)(B * pl.nwg[s]);
     la.inv_cnt[s] = (float)(1.0 / ((double)B * pl.T[s] * (pl.n[s] / 2 + 1)));

@@ -17,7 +17,7 @@ struct MssArgs {
   float* edges;        // (B, n): gradient of the reflect-pad samples, head n/2 then tail n/2
   float* partial;      // (B, nwg, 2): per-workgroup sums of |dS| and |dlogS|
   float* spill;        // (B, nwg, 3n/4): the gradient a workgroup's last three frames put on the
-                       // 3n/4 padded samples past its range (mss_spill_kernel adds them there)
+                       // 3n/4 padded samples past its range (mss_sum_kernel and the edge fold add them)
 };
 
 // n = 2048: grid (nwg, B), 256 threads, one radix-2 step around two fft1024 (fft.hip)
