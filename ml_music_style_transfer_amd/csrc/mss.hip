@@ -462,14 +462,14 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
 }
 
 // ------------------------------------------------------------------ target magnitudes, float64
-// |STFT_n(target)| for every size, frame-major (B, T_n, n/2 + 1), computed in float64 and rounded
-// to float: an fp32 transform leaves bins far below the frame's peak at fp32 rounding noise (a
+// |STFT_n(target)| for every size, frame-major (B, T_n, n/2 + 1): the transform and the power in
+// float64, the power rounded to float and its square root taken in float: an fp32 transform leaves bins far below the frame's peak at fp32 rounding noise (a
 // silent or decaying target's high bins), and log(S + 1e-7) turns that noise into a 1e-3 loss
 // error against the float64 definition (bench_aux's silent piano pair). The target needs no
 // gradient, so it is transformed once per call here and the loss kernels read its magnitudes.
 // One wave transforms FBT = BWT / (n/2) frames at a time in its LDS buffer (n/2-point complex
-// Stockham FFT of z_j = w_2j x_2j + i w_2j+1 x_2j+1, then the real-FFT post-twist), twiddles and
-// window from a compile-time float64 W2048 table.
+// Stockham FFT of z_j = w_2j x_2j + i w_2j+1 x_2j+1, then the real-FFT post-twist), twiddles
+// from a compile-time float64 W2048 table.
 struct MssW2048d {
   double2 w[512];
 };
@@ -501,21 +501,17 @@ __device__ __forceinline__ d2 twd(const d2* qt, int m, int N) {
   return dk(neg ? -a : a, neg ? -b : b);
 }
 
-// LDS slot of complex element i of a wave buffer: slot = i ^ h(i), h linear over bits 3..10 of i
-// (each bit's vector flips only lower bits, so this is a bijection). Found by local search over
-// such swizzles against the ds_read_b128 bank rule (16-lane groups {0-3,12-15,20-27} /
-// {4-11,16-19,28-31}, 16 slots per 256-B row) and the ds_write_b128 rule (8 contiguous lanes, 8
-// slots per 128-B row) for every access of the register-first radix-8 schedule below at n = 64 ..
-// 2048 (tools/lds_swizzle_search.py): 956 modelled conflict cycles over 372 LDS instructions per
-// wave pass of every size, against 1004 over 644 for the round-5 radix-4 schedule with its own
-// searched swizzle. Linear: tsw(a | b) = tsw(a) ^ tsw(b) for disjoint bits, so the loops form one
-// lane-dependent slot and XOR compile-time constants into it.
-__device__ __forceinline__ constexpr int tsw(int i) {
-  constexpr int V[8] = {4, 1, 3, 12, 11, 4, 0, 2};  // bits 3 .. 10
-  int h = 0;
-  for (int b = 0; b < 8; ++b) h ^= (-((i >> (b + 3)) & 1)) & V[b];
-  return i ^ h;
-}
+// LDS slot of complex element i of a wave buffer: i ^ ((i >> 3) & 15) ^ ((i >> 6) & 15) (bits 3..9
+// into bits 0..3; bits 6 and up stay, so bit 3 and then bits 0..2 are recoverable: a bijection).
+// Chosen with the bank model of tools/lds_swizzle_search.py (radix8 mode: ds_read_b128 16-lane
+// groups {0-3,12-15,20-27} / {4-11,16-19,28-31}, 16 slots per 256-B row; ds_write_b128 8
+// contiguous lanes, 8 slots per 128-B row) over every access of the register-first radix-8
+// schedule below at n = 64 .. 2048: 1058 modelled conflict cycles over 372 LDS instructions per
+// wave pass of every size (1174 for one shift-XOR term, 956 for a searched 8-bit XOR map that
+// costs ~24 VALU per address instead of 5; the round-5 radix-4 schedule: 1004 over 644).
+// Linear: tsw(a | b) = tsw(a) ^ tsw(b) for disjoint bits, so the loops form one lane-dependent
+// slot and XOR compile-time constants into it.
+__device__ __forceinline__ constexpr int tsw(int i) { return i ^ ((i >> 3) & 15) ^ ((i >> 6) & 15); }
 
 // a W_R^k for a compile-time k < R / 2 (R | 16): exact forms for 1, -i and (+-1 - i) / sqrt 2
 template <int R>
@@ -710,7 +706,9 @@ __device__ __forceinline__ void mss_target_body(const MssTgt& A, int z, int blk,
         const d2 E = dk(0.5 * (Af.x + Bf.x), 0.5 * (Af.y - Bf.y));
         const d2 D = dk(0.5 * (Af.y + Bf.y), -0.5 * (Af.x - Bf.x));  // -i (A - conj B) / 2
         const d2 X = E + dmul(twd(qt, f, N), D);
-        out[(long long)t * NBIN + f] = (float)sqrt(X.x * X.x + X.y * X.y);
+        // |X| from the float64 power rounded to float, by the hardware square root (1 ulp; the
+        // correctly rounded float64 sqrt is ~15 instructions at the float64 rate)
+        out[(long long)t * NBIN + f] = __builtin_amdgcn_sqrtf((float)(X.x * X.x + X.y * X.y));
       }
     }
     wave_sync();  // the spectra are read before the next batch overwrites the buffer
