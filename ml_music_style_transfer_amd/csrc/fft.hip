@@ -1843,18 +1843,23 @@ __global__ __launch_bounds__(256, 2) void mss_fft2048_kernel(const MssArgs a) {
     }
     if (!grad) continue;
     __syncthreads();
+    // frames th - q (q = 3 .. 0) at offset sp mod H + q H, four fixed steps (mss_wave_body)
     const int r_hi = min(t_round + 2 * W, f_own1);
+    const int s_lo = t_round * H - own_lo, s_hi = (r_hi - 1) * H + N - own_lo;
 #pragma unroll
     for (int i = 0; i < OWN + SPILL; ++i) {
-      const int sp = own_lo + tid + 256 * i;
-      const int th = sp / H;
-      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
+      if (256 * (i + 1) <= s_lo || 256 * i >= s_hi) continue;
+      const unsigned sp = own_lo + tid + 256 * i;
+      const int th = (int)(sp / H);
+      const unsigned jr = sp % H;
       float vv = acc[i];
-      for (int t = t0; t <= t1; ++t) {
-        const int j = sp - t * H;
-        const int rel = t - t_round, ww = rel >> 1;
-        const c2 g = buf[ww * N + j];
-        vv += hann(j) * ((rel & 1) ? g.y : g.x);
+#pragma unroll
+      for (int q = 3; q >= 0; --q) {
+        const int rel = th - q - t_round;
+        const bool ok = rel >= 0 && rel < r_hi - t_round;
+        const unsigned rc = ok ? rel : 0u, j = jr + q * H;
+        const c2 g = buf[(rc >> 1) * N + j];
+        vv = __builtin_fmaf(hann(j), ok ? ((rc & 1) ? g.y : g.x) : 0.f, vv);
       }
       acc[i] = vv;
     }

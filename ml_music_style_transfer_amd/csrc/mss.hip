@@ -404,19 +404,26 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
     }
     if (!grad) continue;  // uniform over the workgroup: no barrier needed
     __syncthreads();      // every wave's gradient frames are in its buffer
-    // windowed overlap-add of the round's frames into the owned samples, frames in order
+    // windowed overlap-add of the round's frames into the owned samples, frames in order. Sample
+    // sp is covered by frames th - q (th = sp / H, q = 3 .. 0) at offset sp mod H + q H: four
+    // fixed steps, a frame outside the round adding 0 (a per-sample loop had divergent trip
+    // counts), over the thread's samples this round's frames reach (a wave-uniform range of i).
     const int r_hi = min(t_round + RF, f_own1);
+    const int s_lo = t_round * H - own_lo, s_hi = (r_hi - 1) * H + N - own_lo;
 #pragma unroll
     for (int i = 0; i < OWN + SPILL; ++i) {
-      const int sp = own_lo + tid + 256 * i;  // padded coordinate
-      const int th = sp / H;
-      const int t0 = max(max(th - 3, t_round), 0), t1 = min(th, r_hi - 1);
+      if (256 * (i + 1) <= s_lo || 256 * i >= s_hi) continue;
+      const unsigned sp = own_lo + tid + 256 * i;  // padded coordinate
+      const int th = (int)(sp / H);
+      const unsigned jr = sp % H;
       float v = acc[i];
-      for (int t = t0; t <= t1; ++t) {
-        const int j = sp - t * H;
-        const int rel = t - t_round, ww = rel / GF, m = (rel - ww * GF) >> 1;
+#pragma unroll
+      for (int q = 3; q >= 0; --q) {
+        const int rel = th - q - t_round;
+        const bool ok = rel >= 0 && rel < r_hi - t_round;
+        const unsigned rc = ok ? rel : 0u, ww = rc / GF, m = (rc % GF) >> 1, j = jr + q * H;
         const c2 g = buf[ww * BW + m * N + j];
-        v += hw[j] * ((rel & 1) ? g.y : g.x);
+        v = __builtin_fmaf(hw[j], ok ? ((rc & 1) ? g.y : g.x) : 0.f, v);
       }
       acc[i] = v;
     }
