@@ -184,6 +184,32 @@ def test_multiscale_spectral_loss_and_grad(cuda, B, L, sizes):
     assert rel <= max(_torch_fp32_mss_grad_gap(p, q, sizes, d64), 1e-3), rel
 
 
+@pytest.mark.parametrize("B,L,sizes", [(2, 4000, (2048, 1024, 512, 256, 128, 64))])
+def test_multiscale_spill_into_tail_pad(cuda, B, L, sizes):
+    """The gradient a workgroup's last frames put past its 4,096 padded samples (the spill slab,
+    mss.hip) where the next range is the clip's tail pad: at L = 4000, n = 2048 and 1024 spill
+    partly past x = L, added by the edge fold's long-clip path (the short-clip fold's spill term
+    is zero whenever it can arise: L <= n + 1 with two ranges means L = 2049, n = 2048, whose
+    last frame ends exactly at the first range's end). Loss within 1e-4; the gradient over
+    x >= L / 2, where every spill lands after the fold, within 1e-4 (relative L2) of the float64
+    oracle (measured 1.6e-5; torch fp32 1.2e-5). The whole gradient is not bounded here: the
+    n = 1024 frame 0 has a bin near zero whose 1 / S factor amplifies fp32 rounding near x = 0
+    (1.1e-2; the round-start build 6.4e-3, torch fp32 3.7e-3; tools/mss_grad_probe.py)."""
+    from ml_music_style_transfer_amd import spectral
+    p, q = _mss_pair(B, L, 11)
+    loss64, d64 = SR.multiscale_spectral_loss_grad(p.astype(np.float64), q.astype(np.float64),
+                                                   1.0, 1e-7, sizes)
+    pt = torch.from_numpy(p).to(cuda).requires_grad_(True)
+    loss = spectral.multiscale_spectral_loss(pt, torch.from_numpy(q).to(cuda), sizes=sizes)
+    loss.backward()
+    assert abs(loss.item() - loss64) <= 1e-4 * abs(loss64)
+    d = pt.grad.cpu().numpy().astype(np.float64)
+    tail = slice(L // 2, L)
+    rel = np.linalg.norm(d[:, tail] - d64[:, tail]) / np.linalg.norm(d64[:, tail])
+    print(f"L={L}: tail-half gradient rel. error {rel:.2e}")
+    assert rel <= 1e-4, rel
+
+
 def _silent_piano_pair(B, L, seed):
     """bench_aux's config-5 recipe: synthetic piano targets (exact silence before the first onset
     and after the last decay) and pred = target + 0.05 N(0, 1)."""
