@@ -204,6 +204,13 @@ __device__ __forceinline__ void stages_f(c2* s, const c2* qt, unsigned lane) {
 #define MST_MSS_OCC 4  // mss_multi_kernel workgroups per CU (launch bound; LDS allows 4)
 #endif
 constexpr int MSS_W = 4;  // waves per workgroup
+#ifdef MSS_STAMPS  // dev instrumentation (tools/micro/mss_stamps.hip): s_memtime per phase, one size
+__device__ unsigned long long g_mss_stamps[2048 * 4 * 4 * 16];
+#define MSTAMP(i) do { if (lane == 0 && flat_wg < 2048 && rnd < 4) \
+    g_mss_stamps[((flat_wg * 4 + wave) * 4 + rnd) * 16 + (i)] = clock64(); } while (0)
+#else
+#define MSTAMP(i) do { } while (0)
+#endif
 template <int LOG2N>
 struct MssGeom {
   static constexpr int N = 1 << LOG2N;
@@ -269,9 +276,14 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
   for (int i = 0; i < OWN + SPILL; ++i) acc[i] = 0.f;
   float s_abs = 0.f, s_log = 0.f;
 
+#ifdef MSS_STAMPS
+  const int flat_wg = w + a.nwg * b;
+  int rnd = 0;
+#endif
 #pragma unroll 1
   for (int t_round = f_lo; t_round < f_own1; t_round += RF) {
     const int t_base = t_round + wave * GF;  // this wave's first frame
+    MSTAMP(0);
     if (t_base < f_own1) {                   // wave-uniform
       c2 zga[NE], zgb[NE];
 #pragma unroll
@@ -322,7 +334,9 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
             for (int r = 0; r < R1; ++r) d[r] = v[r];
           }
           wave_sync();
+          MSTAMP(1 + 3 * pass);
           stages_f<HALF, BW / 2, R1, false>(S, qth, lane);
+          MSTAMP(2 + 3 * pass);
         } else {
           constexpr int KC = 8;  // elements per load batch (2 KC loads in flight)
 #pragma unroll
@@ -345,7 +359,9 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
             }
           }
           wave_sync();
+          MSTAMP(1 + 3 * pass);
           stages_f<HALF, BW / 2, 1, false>(S, qth, lane);
+          MSTAMP(2 + 3 * pass);
         }
         // spectra, loss, gradient spectra (registers)
 #pragma unroll
@@ -380,6 +396,7 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
           else zgb[jj] = zg;
         }
         wave_sync();  // every lane has read the spectra before S is overwritten
+        MSTAMP(3 + 3 * pass);
       }
       if (grad) {
         // C = H^a + i H^b per pair (H^a_f = Za/2, H^a_{n-f} = conj(Za)/2)
@@ -400,10 +417,12 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
         }
         wave_sync();
         stages_f<N, BW, 1, true>(S, qt, lane);
+        MSTAMP(7);
       }
     }
     if (!grad) continue;  // uniform over the workgroup: no barrier needed
     __syncthreads();      // every wave's gradient frames are in its buffer
+    MSTAMP(8);
     // windowed overlap-add of the round's frames into the owned samples, frames in order. Sample
     // sp is covered by frames th - q (th = sp / H, q = 3 .. 0) at offset sp mod H + q H: four
     // fixed steps, a frame outside the round adding 0 (a per-sample loop had divergent trip
@@ -428,6 +447,10 @@ __device__ __forceinline__ void mss_wave_body(const MssArgs& a, int w, int b, ch
       acc[i] = v;
     }
     __syncthreads();  // the buffers are read before the next round overwrites them
+    MSTAMP(9);
+#ifdef MSS_STAMPS
+    ++rnd;
+#endif
   }
 
   s_abs = wave_sum(s_abs);
